@@ -1,0 +1,669 @@
+// render.hip — the gfx950 path-tracing megakernel and its host driver.
+//
+// Replaces cpu_ray_tracer/tracer.rs:160-219 (save_image + recursive get_color)
+// and the shapes/ hit/scatter code it calls. One lane owns one pixel for all of
+// its samples, so the per-pixel f32 sum runs in sample order exactly as
+// `col = col + get_color(...)` does (tracer.rs:170-175). A lane whose path ends
+// immediately starts its next sample (path regeneration), so no lane idles while
+// its wave still has work. The attenuation product is unwound right-to-left from
+// a per-lane LDS stack, reproducing the recursion's association
+// a0*(a1*(...*terminal)) bit for bit.
+//
+// Scene data is wave-uniform inside the closest-hit loop (every lane tests
+// primitive i at the same time): the kind switch is a scalar branch and the
+// geometry arrives by scalar loads. Layout and rooflines: DESIGN.md §4-§5.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <string.h>
+#include <chrono>
+#include <thread>
+
+#include "internal.h"
+#include "rt_core.h"
+
+#define HIPCHK(call)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fr::set_error(FR_EHIP, "%s failed: %s", #call, hipGetErrorString(e_));       \
+  } while (0)
+
+namespace fr {
+
+constexpr uint32_t kBlock = 256;      // 4 waves, one 8x8 pixel tile each
+constexpr uint32_t kStripRows = 8;    // rows per shard strip == tile height
+constexpr uint32_t kMaxDepth = 64;    // LDS stack bound (64 KB per workgroup)
+
+// ABI layout, mirrored by ctypes (forma_rt.py) and the Rust binding
+static_assert(sizeof(fr_prim) == 88, "fr_prim layout");
+static_assert(sizeof(fr_camera) == 104, "fr_camera layout");
+static_assert(sizeof(fr_params) == 40, "fr_params layout");
+static_assert(sizeof(fr_stats) == 48, "fr_stats layout");
+
+struct DeviceCopy {
+  int device = -1;
+  uint64_t version = 0;
+  void* blob = nullptr;
+  uint32_t n = 0;
+  size_t off_kind = 0, off_g0 = 0, off_g1 = 0, off_g2 = 0, off_g3 = 0, off_mat = 0, off_cls = 0, off_att = 0;
+};
+
+struct KScene {
+  const uint32_t* __restrict__ kind;
+  const float4* __restrict__ g0;
+  const float4* __restrict__ g1;
+  const float4* __restrict__ g2;
+  const float4* __restrict__ g3;
+  const float4* __restrict__ mat;   // colour rgb, fuzz
+  const uint32_t* __restrict__ cls; // effective ScatterClass
+  const float4* __restrict__ att;   // attenuation rgb (colour, or 1 for light)
+  uint32_t n;
+};
+
+struct KParams {
+  uint32_t W, H, spp, max_depth;
+  uint64_t seed;
+  uint32_t shard_index, shard_count, tiles_per_row, n_tiles, flags;
+};
+
+// camera.rs fields the ray generator reads: position, lower_left_corner,
+// horizontal, vertical, u, v (named b* here), lens_radius
+struct KCam {
+  float px, py, pz, lx, ly, lz, hx, hy, hz, vx, vy, vz, ux, uy, uz, bx, by, bz, lens;
+};
+
+// Effective scatter class after each shape's fallback chain
+// (sphere.rs:56-69: 0/1/2/3 else lambertian; plane.rs:48-59: 1 metal else lambertian).
+static uint32_t scatter_class(const fr_prim& p) {
+  if (p.kind == FR_STUB) return SC_NONE;
+  if (p.kind == FR_PLANE) return p.material == FR_METAL ? SC_METAL : SC_LAMBERT;
+  switch (p.material) {
+    case FR_METAL: return SC_METAL;
+    case FR_DIELECTRIC: return SC_DIELECTRIC;
+    case FR_LIGHT: return SC_LIGHT;
+    default: return SC_LAMBERT;
+  }
+}
+
+__device__ __forceinline__ V3 xyz(float4 a) { return V3{a.x, a.y, a.z}; }
+
+__global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KParams kp,
+                                                        float* __restrict__ out_mean,
+                                                        uint8_t* __restrict__ out_u8,
+                                                        unsigned long long* __restrict__ counters) {
+  extern __shared__ uint32_t stack[];  // [max_depth][kBlock] primitive indices
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u;
+  const uint32_t tile = blockIdx.x * (kBlock / 64u) + (tid >> 6);
+
+  uint32_t x = 0, y = 0;
+  bool valid = false;
+  if (tile < kp.n_tiles) {
+    const uint32_t ls = tile / kp.tiles_per_row;
+    const uint32_t tc = tile - ls * kp.tiles_per_row;
+    const uint32_t strip = kp.shard_index + ls * kp.shard_count;
+    x = tc * 8u + (lane & 7u);
+    y = strip * kStripRows + (lane >> 3);
+    valid = x < kp.W && y < kp.H;
+  }
+  const uint32_t pixel = y * kp.W + x;
+  const V3 cpos{cam.px, cam.py, cam.pz}, cllc{cam.lx, cam.ly, cam.lz}, chor{cam.hx, cam.hy, cam.hz};
+  const V3 cver{cam.vx, cam.vy, cam.vz}, cu{cam.ux, cam.uy, cam.uz}, cv{cam.bx, cam.by, cam.bz};
+  const float fW = static_cast<float>(kp.W), fH = static_cast<float>(kp.H);
+  const float fx = static_cast<float>(x), fy = static_cast<float>(kp.H - y);  // tracer.rs:171-172
+
+  V3 sum{0.0f, 0.0f, 0.0f};
+  V3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
+  Rng rng{0u, 0u, 0u, 0u};
+  uint32_t s = 0, depth = 0, nseg = 0, nhit = 0;
+  bool alive = false;
+  bool todo = valid && kp.spp > 0;
+
+  while (todo) {
+    if (!alive) {
+      // start sample s: jitter, then Camera::get_ray (camera.rs:62-72)
+      rng = rng_seed(kp.seed, pixel, s);
+      const float r0 = rng_f32(rng);
+      const float r1 = rng_f32(rng);
+      const float u = (fx + r0) / fW;
+      const float v = (fy + r1) / fH;
+      const V3 rd = scl(cam.lens, random_in_unit_circle(rng));
+      const V3 off = add(scl(rd.x, cu), scl(rd.y, cv));
+      o = add(cpos, off);
+      d = sub(sub(add(add(cllc, scl(u, chor)), scl(v, cver)), cpos), off);
+      depth = 0;
+      alive = true;
+    }
+    ++nseg;
+    // closest hit over the list in order (tracer.rs:190-200); one shared record
+    HitRec rec{0.0f, V3{0.0f, 0.0f, 0.0f}, V3{0.0f, 0.0f, 0.0f}};
+    float closest = FLT_MAX;
+    int best = -1;
+    const V3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    for (uint32_t i = 0; i < sc.n; ++i) {
+      const uint32_t k = sc.kind[i];
+      bool h;
+      if (k == FR_AABB) {
+        h = hit_aabb(xyz(sc.g0[i]), xyz(sc.g1[i]), o, d, inv, 0.001f, closest, rec);
+      } else if (k == FR_SPHERE) {
+        const float4 g = sc.g0[i];
+        h = hit_sphere(xyz(g), g.w, o, d, 0.001f, closest, rec);
+      } else if (k == FR_PLANE) {
+        h = hit_plane(xyz(sc.g0[i]), xyz(sc.g1[i]), xyz(sc.g2[i]), o, d, 0.001f, closest, rec);
+      } else if (k == FR_OBB) {
+        const float4 a = sc.g0[i], b = sc.g1[i], c = sc.g2[i], e = sc.g3[i];
+        h = hit_obb(xyz(a), xyz(b), xyz(c), xyz(e), V3{a.w, b.w, c.w}, o, d, 0.001f, closest, rec);
+      } else {
+        h = false;  // shapes/aabb.rs, rectangle.rs stubs
+      }
+      if (h) {
+        closest = rec.t;
+        best = static_cast<int>(i);
+      }
+    }
+
+    V3 term;
+    if (best >= 0) {
+      ++nhit;
+      if (depth < kp.max_depth) {
+        const uint32_t c = sc.cls[best];
+        bool ok = true;
+        V3 nd;
+        if (c == SC_METAL) {
+          ok = scatter_metal(d, rec.p, rec.n, sc.mat[best].w, rng, nd);
+        } else if (c == SC_DIELECTRIC) {
+          nd = scatter_dielectric(d, rec.n, rng);
+        } else if (c == SC_NONE) {
+          ok = false;
+        } else {
+          nd = scatter_lambert(rec.p, rec.n, rng);
+        }
+        if (ok) {
+          stack[depth * kBlock + tid] = static_cast<uint32_t>(best);
+          ++depth;
+          o = rec.p;
+          d = nd;
+          continue;
+        }
+      }
+      term = V3{0.0f, 0.0f, 0.0f};
+    } else {
+      term = sky(d);
+    }
+    // attenuation * get_color(...) (tracer.rs:206-207), innermost first
+    V3 col = term;
+    for (int j = static_cast<int>(depth) - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
+    sum = add(sum, col);
+    alive = false;
+    if (++s == kp.spp) todo = false;
+  }
+
+  if (valid) {
+    const V3 mean = divs(sum, static_cast<float>(kp.spp));  // tracer.rs:177
+    const size_t idx = static_cast<size_t>(pixel) * 3u;
+    out_mean[idx + 0] = mean.x;
+    out_mean[idx + 1] = mean.y;
+    out_mean[idx + 2] = mean.z;
+    if (kp.flags & FR_FLAG_WRITE_U8) {
+      out_u8[idx + 0] = to_u8(mean.x);
+      out_u8[idx + 1] = to_u8(mean.y);
+      out_u8[idx + 2] = to_u8(mean.z);
+    }
+  }
+  // per-wave counter reduction, one 64-bit atomic per wave per counter
+  unsigned long long a = nseg, b = nhit;
+  for (int m = 32; m > 0; m >>= 1) {
+    a += __shfl_xor(a, m);
+    b += __shfl_xor(b, m);
+  }
+  if (lane == 0 && (a | b)) {
+    atomicAdd(&counters[0], a);
+    atomicAdd(&counters[1], b);
+  }
+}
+
+// ---- diagnostics kernels ---------------------------------------------------
+
+__global__ void ops_kernel(int op, const float* a, const float* b, uint32_t n, float* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x = a[i], y = b[i];
+  float r;
+  switch (op) {
+    case 0: r = x + y; break;
+    case 1: r = x - y; break;
+    case 2: r = x * y; break;
+    case 3: r = x / y; break;
+    case 4: r = sqrtf(x); break;
+    case 5: r = schlick(x, y); break;
+    case 6: r = static_cast<float>(to_u8(x)); break;
+    case 7: r = unit(V3{x, y, 1.0f}).x; break;
+    case 8: r = 1.0f / x; break;
+    default: r = 0.0f;
+  }
+  out[i] = r;
+}
+
+__global__ void rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  Rng r = rng_seed(seed, pixel, sample);
+  for (uint32_t i = 0; i < n; ++i) out[i] = rng_next(r);
+}
+
+// ---- device scene copies ----------------------------------------------------
+
+static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
+  std::lock_guard<std::mutex> g(s->mu);
+  for (DeviceCopy* c : s->copies)
+    if (c->device == device) {
+      if (c->version == s->version) {
+        *out = c;
+        return FR_OK;
+      }
+      HIPCHK(hipFree(c->blob));
+      c->blob = nullptr;
+    }
+  DeviceCopy* c = nullptr;
+  for (DeviceCopy* e : s->copies)
+    if (e->device == device) c = e;
+  if (!c) {
+    c = new DeviceCopy();
+    c->device = device;
+    s->copies.push_back(c);
+  }
+  const uint32_t n = static_cast<uint32_t>(s->prims.size());
+  const size_t m = n ? n : 1;  // never hand the kernel a null array
+  size_t off = 0;
+  c->off_kind = off;
+  off = align_up(off + m * 4, 256);
+  c->off_g0 = off;
+  off = align_up(off + m * 16, 256);
+  c->off_g1 = off;
+  off = align_up(off + m * 16, 256);
+  c->off_g2 = off;
+  off = align_up(off + m * 16, 256);
+  c->off_g3 = off;
+  off = align_up(off + m * 16, 256);
+  c->off_mat = off;
+  off = align_up(off + m * 16, 256);
+  c->off_cls = off;
+  off = align_up(off + m * 4, 256);
+  c->off_att = off;
+  off = align_up(off + m * 16, 256);
+  std::vector<unsigned char> host(off, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    const fr_prim& p = s->prims[i];
+    uint32_t kind = p.kind;
+    float4 g[4] = {};
+    switch (p.kind) {
+      case FR_SPHERE: g[0] = make_float4(p.g[0], p.g[1], p.g[2], p.g[3]); break;
+      case FR_AABB:
+        g[0] = make_float4(p.g[0], p.g[1], p.g[2], 0.0f);
+        g[1] = make_float4(p.g[3], p.g[4], p.g[5], 0.0f);
+        break;
+      case FR_PLANE:
+        g[0] = make_float4(p.g[0], p.g[1], p.g[2], 0.0f);
+        g[1] = make_float4(p.g[3], p.g[4], p.g[5], 0.0f);
+        g[2] = make_float4(p.g[6], p.g[7], p.g[8], 0.0f);
+        break;
+      case FR_OBB:
+        g[0] = make_float4(p.g[0], p.g[1], p.g[2], p.g[12]);
+        g[1] = make_float4(p.g[3], p.g[4], p.g[5], p.g[13]);
+        g[2] = make_float4(p.g[6], p.g[7], p.g[8], p.g[14]);
+        g[3] = make_float4(p.g[9], p.g[10], p.g[11], 0.0f);
+        break;
+      default: kind = FR_STUB;
+    }
+    const uint32_t cls = scatter_class(p);
+    const float4 mat = make_float4(p.color[0], p.color[1], p.color[2], p.fuzz);
+    const float4 att = cls == SC_LIGHT ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
+                                       : make_float4(p.color[0], p.color[1], p.color[2], 0.0f);
+    memcpy(&host[c->off_kind + 4 * i], &kind, 4);
+    memcpy(&host[c->off_g0 + 16 * i], &g[0], 16);
+    memcpy(&host[c->off_g1 + 16 * i], &g[1], 16);
+    memcpy(&host[c->off_g2 + 16 * i], &g[2], 16);
+    memcpy(&host[c->off_g3 + 16 * i], &g[3], 16);
+    memcpy(&host[c->off_mat + 16 * i], &mat, 16);
+    memcpy(&host[c->off_cls + 4 * i], &cls, 4);
+    memcpy(&host[c->off_att + 16 * i], &att, 16);
+  }
+  if (n == 0) {
+    const uint32_t stub = FR_STUB;
+    memcpy(&host[c->off_kind], &stub, 4);
+  }
+  HIPCHK(hipMalloc(&c->blob, off));
+  HIPCHK(hipMemcpy(c->blob, host.data(), off, hipMemcpyHostToDevice));
+  c->n = n;
+  c->version = s->version;
+  *out = c;
+  return FR_OK;
+}
+
+void release_device_copies(fr_scene* s) {
+  std::lock_guard<std::mutex> g(s->mu);
+  for (DeviceCopy* c : s->copies) {
+    if (c->blob) {
+      int cur = 0;
+      if (hipGetDevice(&cur) == hipSuccess) {
+        (void)hipSetDevice(c->device);
+        (void)hipFree(c->blob);
+        (void)hipSetDevice(cur);
+      }
+    }
+    delete c;
+  }
+  s->copies.clear();
+}
+
+}  // namespace fr
+
+using namespace fr;
+
+struct fr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float* d_mean = nullptr;
+  uint8_t* d_u8 = nullptr;
+  unsigned long long* d_cnt = nullptr;
+  size_t cap_pixels = 0;
+  fr_params last{};
+  uint32_t last_n = 0;
+  bool pending = false;
+  std::chrono::steady_clock::time_point t0;
+};
+
+static int check_params(const fr_params* p) {
+  if (!p) return set_error(FR_EARG, "null params");
+  if (p->width == 0 || p->height == 0) return set_error(FR_EARG, "width/height must be > 0");
+  if (static_cast<uint64_t>(p->width) * p->height > (1ull << 31))
+    return set_error(FR_EARG, "image too large (pixel index must fit in 31 bits)");
+  if (p->max_depth > kMaxDepth) return set_error(FR_EARG, "max_depth %u > %u", p->max_depth, kMaxDepth);
+  if (p->strip_rows != kStripRows) return set_error(FR_EARG, "strip_rows must be %u", kStripRows);
+  if (p->shard_count == 0 || p->shard_index >= p->shard_count)
+    return set_error(FR_EARG, "shard_index %u / shard_count %u invalid", p->shard_index, p->shard_count);
+  return FR_OK;
+}
+
+extern "C" {
+
+int fr_device_count(int* count) {
+  if (!count) return set_error(FR_EARG, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return set_error(FR_ENODEV, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *count = n;
+  return FR_OK;
+}
+
+int fr_ctx_create(int device, void* stream, fr_ctx** out) {
+  if (!out) return set_error(FR_EARG, "fr_ctx_create: null output");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_error(FR_ENODEV, "no HIP device");
+  if (device < 0 || device >= n) return set_error(FR_ENODEV, "device %d not present (%d devices)", device, n);
+  HIPCHK(hipSetDevice(device));
+  fr_ctx* c = new fr_ctx();
+  c->device = device;
+  if (stream) {
+    c->stream = static_cast<hipStream_t>(stream);
+  } else {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      return set_error(FR_EHIP, "hipStreamCreate failed");
+    }
+    c->own_stream = true;
+  }
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipMalloc(&c->d_cnt, 4 * sizeof(unsigned long long)) != hipSuccess) {
+    fr_ctx_free(c);
+    return set_error(FR_EHIP, "fr_ctx_create: event/counter allocation failed");
+  }
+  *out = c;
+  return FR_OK;
+}
+
+void fr_ctx_free(fr_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->d_mean) (void)hipFree(c->d_mean);
+  if (c->d_u8) (void)hipFree(c->d_u8);
+  if (c->d_cnt) (void)hipFree(c->d_cnt);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_params* p) {
+  if (!c || !scene || !cam) return set_error(FR_EARG, "fr_ctx_render: null argument");
+  int rc = check_params(p);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(c->device));
+  DeviceCopy* dc = nullptr;
+  rc = upload_scene(scene, c->device, &dc);
+  if (rc) return rc;
+  const size_t pixels = static_cast<size_t>(p->width) * p->height;
+  if (pixels > c->cap_pixels) {
+    if (c->d_mean) HIPCHK(hipFree(c->d_mean));
+    if (c->d_u8) HIPCHK(hipFree(c->d_u8));
+    c->d_mean = nullptr;
+    c->d_u8 = nullptr;
+    c->cap_pixels = 0;
+    HIPCHK(hipMalloc(&c->d_mean, pixels * 3 * sizeof(float)));
+    HIPCHK(hipMalloc(&c->d_u8, pixels * 3));
+    c->cap_pixels = pixels;
+  }
+  KScene ks;
+  const char* b = static_cast<const char*>(dc->blob);
+  ks.kind = reinterpret_cast<const uint32_t*>(b + dc->off_kind);
+  ks.g0 = reinterpret_cast<const float4*>(b + dc->off_g0);
+  ks.g1 = reinterpret_cast<const float4*>(b + dc->off_g1);
+  ks.g2 = reinterpret_cast<const float4*>(b + dc->off_g2);
+  ks.g3 = reinterpret_cast<const float4*>(b + dc->off_g3);
+  ks.mat = reinterpret_cast<const float4*>(b + dc->off_mat);
+  ks.cls = reinterpret_cast<const uint32_t*>(b + dc->off_cls);
+  ks.att = reinterpret_cast<const float4*>(b + dc->off_att);
+  ks.n = dc->n;
+  KCam kc{cam->position[0], cam->position[1], cam->position[2], cam->lower_left[0], cam->lower_left[1],
+          cam->lower_left[2], cam->horizontal[0], cam->horizontal[1], cam->horizontal[2], cam->vertical[0],
+          cam->vertical[1], cam->vertical[2], cam->u[0], cam->u[1], cam->u[2], cam->v[0], cam->v[1], cam->v[2],
+          cam->lens_radius};
+  KParams kp;
+  kp.W = p->width;
+  kp.H = p->height;
+  kp.spp = p->spp;
+  kp.max_depth = p->max_depth;
+  kp.seed = p->seed;
+  kp.shard_index = p->shard_index;
+  kp.shard_count = p->shard_count;
+  kp.flags = p->flags;
+  kp.tiles_per_row = (p->width + 7u) / 8u;
+  const uint32_t strips = (p->height + kStripRows - 1) / kStripRows;
+  const uint32_t my_strips =
+      strips > p->shard_index ? (strips - p->shard_index + p->shard_count - 1) / p->shard_count : 0u;
+  kp.n_tiles = my_strips * kp.tiles_per_row;
+  c->t0 = std::chrono::steady_clock::now();
+  HIPCHK(hipMemsetAsync(c->d_cnt, 0, 4 * sizeof(unsigned long long), c->stream));
+  HIPCHK(hipEventRecord(c->ev0, c->stream));
+  if (kp.n_tiles) {
+    const uint32_t blocks = (kp.n_tiles + 3u) / 4u;
+    const size_t lds = static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock * sizeof(uint32_t);
+    hipLaunchKernelGGL(trace_kernel, dim3(blocks), dim3(kBlock), lds, c->stream, ks, kc, kp, c->d_mean, c->d_u8,
+                       c->d_cnt);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  c->last = *p;
+  c->last_n = dc->n;
+  c->pending = true;
+  return FR_OK;
+}
+
+int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
+  if (!c) return set_error(FR_EARG, "fr_ctx_sync: null ctx");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (!c->pending) return set_error(FR_EARG, "fr_ctx_sync: nothing rendered");
+  if (st) {
+    unsigned long long cnt[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpy(cnt, c->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    const fr_params& p = c->last;
+    const uint32_t strips = (p.height + kStripRows - 1) / kStripRows;
+    uint64_t rows = 0;
+    for (uint32_t k = p.shard_index; k < strips; k += p.shard_count) {
+      const uint32_t r0 = k * kStripRows, r1 = r0 + kStripRows < p.height ? r0 + kStripRows : p.height;
+      rows += r1 - r0;
+    }
+    st->segments = cnt[0];
+    st->hits = cnt[1];
+    st->samples = rows * p.width * static_cast<uint64_t>(p.spp);
+    st->prim_tests = cnt[0] * static_cast<uint64_t>(c->last_n);
+    st->kernel_ms = ms;
+    st->total_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t0).count();
+  }
+  return FR_OK;
+}
+
+int fr_ctx_download(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
+  if (!c || !c->pending) return set_error(FR_EARG, "fr_ctx_download: nothing rendered");
+  HIPCHK(hipSetDevice(c->device));
+  const fr_params& p = c->last;
+  const uint32_t strips = (p.height + kStripRows - 1) / kStripRows;
+  const size_t row_f = static_cast<size_t>(p.width) * 3;  // elements per row
+  // full strips of this shard form a strided 2-D region; the trailing partial strip is separate
+  uint32_t full = 0, partial = 0;
+  for (uint32_t k = p.shard_index; k < strips; k += p.shard_count) {
+    if ((k + 1) * kStripRows <= p.height)
+      ++full;
+    else
+      partial = k;
+  }
+  const size_t first = static_cast<size_t>(p.shard_index) * kStripRows * row_f;
+  const size_t pitch = static_cast<size_t>(p.shard_count) * kStripRows * row_f;
+  const size_t width = kStripRows * row_f;
+  const bool has_partial = (p.height % kStripRows) != 0 && (strips - 1) % p.shard_count == p.shard_index;
+  if (mean_rgb) {
+    if (full)
+      HIPCHK(hipMemcpy2DAsync(mean_rgb + first, pitch * 4, c->d_mean + first, pitch * 4, width * 4, full,
+                              hipMemcpyDeviceToHost, c->stream));
+    if (has_partial) {
+      const size_t o = static_cast<size_t>(partial) * kStripRows * row_f;
+      HIPCHK(hipMemcpyAsync(mean_rgb + o, c->d_mean + o, (p.height - partial * kStripRows) * row_f * 4,
+                            hipMemcpyDeviceToHost, c->stream));
+    }
+  }
+  if (rgb8) {
+    if (full)
+      HIPCHK(hipMemcpy2DAsync(rgb8 + first, pitch, c->d_u8 + first, pitch, width, full, hipMemcpyDeviceToHost,
+                              c->stream));
+    if (has_partial) {
+      const size_t o = static_cast<size_t>(partial) * kStripRows * row_f;
+      HIPCHK(hipMemcpyAsync(rgb8 + o, c->d_u8 + o, (p.height - partial * kStripRows) * row_f,
+                            hipMemcpyDeviceToHost, c->stream));
+    }
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return FR_OK;
+}
+
+int fr_ctx_device_buffers(fr_ctx* c, float** d_mean, uint8_t** d_u8) {
+  if (!c) return set_error(FR_EARG, "fr_ctx_device_buffers: null ctx");
+  if (d_mean) *d_mean = c->d_mean;
+  if (d_u8) *d_u8 = c->d_u8;
+  return FR_OK;
+}
+
+int fr_render_hip(fr_scene* scene, const fr_camera* cam, const fr_params* params, int device, float* mean_rgb,
+                  uint8_t* rgb8, fr_stats* stats) {
+  fr_ctx* c = nullptr;
+  int rc = fr_ctx_create(device, nullptr, &c);
+  if (rc) return rc;
+  fr_params p = *params;
+  if (rgb8) p.flags |= FR_FLAG_WRITE_U8;
+  rc = fr_ctx_render(c, scene, cam, &p);
+  if (!rc) rc = fr_ctx_sync(c, stats);
+  if (!rc) rc = fr_ctx_download(c, mean_rgb, rgb8);
+  fr_ctx_free(c);
+  return rc;
+}
+
+int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* params, int n_gpus,
+                        float* mean_rgb, uint8_t* rgb8, fr_stats* stats) {
+  if (!params || n_gpus < 1) return set_error(FR_EARG, "fr_render_hip_multi: bad arguments");
+  int avail = 0;
+  if (hipGetDeviceCount(&avail) != hipSuccess || avail < n_gpus)
+    return set_error(FR_ENODEV, "fr_render_hip_multi: %d devices requested, %d present", n_gpus, avail);
+  // Upload on the calling thread first so the per-device threads only read the scene.
+  std::vector<int> rcs(n_gpus, 0);
+  std::vector<fr_stats> sts(n_gpus);
+  std::vector<std::string> errs(n_gpus);
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  for (int g = 0; g < n_gpus; ++g) {
+    th.emplace_back([&, g]() {
+      fr_params p = *params;
+      p.shard_index = static_cast<uint32_t>(g);
+      p.shard_count = static_cast<uint32_t>(n_gpus);
+      rcs[g] = fr_render_hip(scene, cam, &p, g, mean_rgb, rgb8, &sts[g]);
+      if (rcs[g]) errs[g] = fr_last_error();
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int g = 0; g < n_gpus; ++g)
+    if (rcs[g]) return set_error(rcs[g], "device %d: %s", g, errs[g].c_str());
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    for (int g = 0; g < n_gpus; ++g) {
+      stats->segments += sts[g].segments;
+      stats->hits += sts[g].hits;
+      stats->samples += sts[g].samples;
+      stats->prim_tests += sts[g].prim_tests;
+      if (sts[g].kernel_ms > stats->kernel_ms) stats->kernel_ms = sts[g].kernel_ms;
+    }
+    stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return FR_OK;
+}
+
+int fr_selftest_ops(int device, int op, const float* a, const float* b, uint32_t n, float* out) {
+  if (!a || !b || !out) return set_error(FR_EARG, "fr_selftest_ops: null buffer");
+  HIPCHK(hipSetDevice(device));
+  float *da = nullptr, *db = nullptr, *dout = nullptr;
+  const size_t bytes = (n ? n : 1) * sizeof(float);
+  HIPCHK(hipMalloc(&da, bytes));
+  HIPCHK(hipMalloc(&db, bytes));
+  HIPCHK(hipMalloc(&dout, bytes));
+  HIPCHK(hipMemcpy(da, a, n * sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(db, b, n * sizeof(float), hipMemcpyHostToDevice));
+  if (n) hipLaunchKernelGGL(ops_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, op, da, db, n, dout);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, n * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(da));
+  HIPCHK(hipFree(db));
+  HIPCHK(hipFree(dout));
+  return FR_OK;
+}
+
+int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
+  if (!out) return set_error(FR_EARG, "fr_selftest_rng: null buffer");
+  HIPCHK(hipSetDevice(device));
+  uint32_t* d = nullptr;
+  HIPCHK(hipMalloc(&d, (n ? n : 1) * sizeof(uint32_t)));
+  hipLaunchKernelGGL(rng_kernel, dim3(1), dim3(64), 0, 0, seed, pixel, sample, n, d);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, d, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(d));
+  return FR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,351 @@
+// rt_core.h — f32 arithmetic of fo-rma's tracer hot path, shared by the gfx950
+// kernel and the host-side camera setup of libforma_rt.
+//
+// Every expression keeps the reference's IEEE-f32 operation order, because path
+// tracing is chaotic: one ulp in a hit distance or a rejection test changes the
+// whole path. Build rules (enforced in the Makefile): -ffp-contract=off, no
+// fast-math, correctly rounded '/' and sqrt on the device, no denormal flush.
+//
+// Reference mapping (paths relative to the reference root):
+//   V3 ops ............ cpu_ray_tracer/primitives.rs:50-150 (dot :58-60, cross :62-68,
+//                       unit_vector :70-72)
+//   reflect/refract/schlick ... cpu_ray_tracer/utility.rs:27-54
+//   random_in_unit_{circle,sphere} ... utility.rs:4-25 (rejection loops)
+//   Rng ............... replaces rand::thread_rng() (rand 0.9.2, Cargo.lock:2735) with a
+//                       counter-keyed xoshiro128** stream per (seed, pixel, sample)
+//   hit_sphere ........ shapes/sphere.rs:23-51
+//   hit_plane ......... shapes/plane.rs:24-44 (stale-record quirk kept)
+//   hit_aabb/hit_obb .. build-defined box, shaped like Sphere::hit
+//   scatter_* ......... shapes/sphere.rs:84-152, shapes/plane.rs:101-122
+//   sky ............... cpu_ray_tracer/tracer.rs:211-218
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define FR_HD __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#define FR_HD static inline
+#endif
+
+namespace fr {
+
+struct V3 {
+  float x, y, z;
+};
+
+FR_HD V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+FR_HD V3 add(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+FR_HD V3 sub(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+FR_HD V3 mul(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+// f32 * Vec3 (primitives.rs:128-138) and Vec3 * f32 (:116-126) are the same products.
+FR_HD V3 scl(float s, V3 a) { return V3{s * a.x, s * a.y, s * a.z}; }
+FR_HD V3 divs(V3 a, float s) { return V3{a.x / s, a.y / s, a.z / s}; }
+// primitives.rs:58-60 — left to right, no fused multiply-add
+FR_HD float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+FR_HD V3 cross(V3 a, V3 b) {
+  return V3{a.y * b.z - a.z * b.y, -(a.x * b.z - a.z * b.x), a.x * b.y - a.y * b.x};
+}
+FR_HD float length(V3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
+FR_HD V3 unit(V3 a) { return divs(a, length(a)); }  // 3 divides, no reciprocal
+
+// utility.rs:27-30: v - 2*dot(v,n)*n, evaluated as v - ((2*dot) * n)
+FR_HD V3 reflect(V3 v, V3 n) { return sub(v, scl(2.0f * dot(v, n), n)); }
+
+// utility.rs:49-54; powi(x,5) is lowered by LLVM's ExpandPowI (and compiler-rt's
+// __powisf2) to x * ((x*x)*(x*x)); frozen here.
+FR_HD float schlick(float cosine, float ref_idx) {
+  float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+  r0 = r0 * r0;
+  float x = 1.0f - cosine;
+  float x2 = x * x;
+  float x4 = x2 * x2;
+  return r0 + (1.0f - r0) * (x * x4);
+}
+
+// ---------------------------------------------------------------------------
+// RNG. One stream per (seed, pixel, sample): splitmix64 keys a xoshiro128**
+// state; f32 = (u32 >> 8) * 2^-24, the documented mapping of rand's f32 sampling.
+// ---------------------------------------------------------------------------
+struct Rng {
+  uint32_t s0, s1, s2, s3;
+};
+
+FR_HD uint64_t splitmix64_next(uint64_t& x) {
+  x += 0x9E3779B97F4A7C15ull;
+  uint64_t z = x;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+FR_HD Rng rng_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {
+  uint64_t x = seed ^ ((static_cast<uint64_t>(pixel) << 32) | static_cast<uint64_t>(sample));
+  uint64_t a = splitmix64_next(x);
+  uint64_t b = splitmix64_next(x);
+  return Rng{static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
+             static_cast<uint32_t>(b >> 32)};
+}
+
+FR_HD uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+
+FR_HD uint32_t rng_next(Rng& r) {  // xoshiro128** 1.1
+  const uint32_t result = rotl32(r.s1 * 5u, 7) * 9u;
+  const uint32_t t = r.s1 << 9;
+  r.s2 ^= r.s0;
+  r.s3 ^= r.s1;
+  r.s1 ^= r.s2;
+  r.s0 ^= r.s3;
+  r.s2 ^= t;
+  r.s3 = rotl32(r.s3, 11);
+  return result;
+}
+
+// u in [0, 2^24) scaled by 2^-24: exact, in [0, 1)
+FR_HD float rng_f32(Rng& r) { return static_cast<float>(rng_next(r) >> 8) * 5.9604644775390625e-08f; }
+
+// 2*r - 1 for r = k*2^-24 is exactly (k - 2^23) * 2^-23 (both sides exact in f32),
+// so one integer subtract replaces the reference's two float ops bit for bit.
+FR_HD float rng_signed_unit(Rng& r) {
+  return static_cast<float>(static_cast<int32_t>(rng_next(r) >> 8) - 8388608) * 1.1920928955078125e-07f;
+}
+
+// utility.rs:4-13: p = 2*(r1, r2, 0) - (1, 1, 0), retry while dot(p,p) >= 1
+FR_HD V3 random_in_unit_circle(Rng& r) {
+  float px, py;
+  do {
+    px = rng_signed_unit(r);
+    py = rng_signed_unit(r);
+    // dot(p,p) = (px*px + py*py) + 0*0; adding +0 to a sum of squares is exact
+  } while (px * px + py * py >= 1.0f);
+  return V3{px, py, 0.0f};
+}
+
+// utility.rs:15-25: p = 2*(r1, r2, r3) - (1, 1, 1), retry while dot(p,p) >= 1
+FR_HD V3 random_in_unit_sphere(Rng& r) {
+  float px, py, pz;
+  do {
+    px = rng_signed_unit(r);
+    py = rng_signed_unit(r);
+    pz = rng_signed_unit(r);
+  } while (px * px + py * py + pz * pz >= 1.0f);
+  return V3{px, py, pz};
+}
+
+// ---------------------------------------------------------------------------
+// Hit record / primitives
+// ---------------------------------------------------------------------------
+struct HitRec {
+  float t;
+  V3 p;
+  V3 n;
+};
+
+// shapes/sphere.rs:23-51
+FR_HD bool hit_sphere(V3 c, float radius, V3 o, V3 d, float t_min, float t_max, HitRec& rec) {
+  const V3 oc = sub(o, c);
+  const float a = dot(d, d);
+  const float b = dot(oc, d);
+  const float cc = dot(oc, oc) - radius * radius;
+  const float disc = b * b - a * cc;
+  if (disc > 0.0f) {
+    const float sq = sqrtf(disc);
+    const float r1 = (-b - sq) / a;
+    if (r1 > t_min && r1 < t_max) {
+      rec.t = r1;
+      rec.p = add(o, scl(r1, d));
+      rec.n = divs(sub(rec.p, c), radius);
+      return true;
+    }
+    const float r2 = (-b + sq) / a;
+    if (r2 > t_min && r2 < t_max) {
+      rec.t = r2;
+      rec.p = add(o, scl(r2, d));
+      rec.n = divs(sub(rec.p, c), radius);
+      return true;
+    }
+  }
+  return false;
+}
+
+// shapes/plane.rs:24-44 — denom is compared against the t-range; t and p are
+// written before the bounds test (a failed test leaves them stale); t may be < 0.
+FR_HD bool hit_plane(V3 pos, V3 orient, V3 size, V3 o, V3 d, float t_min, float t_max, HitRec& rec) {
+  const float denom = dot(orient, d);
+  if (denom > t_min && denom < t_max) {
+    const V3 ptr = sub(pos, o);
+    rec.t = dot(ptr, orient) / denom;
+    rec.p = add(o, scl(rec.t, d));
+    if (rec.p.x > pos.x - size.x && rec.p.x < pos.x + size.x && rec.p.y > pos.y - size.y &&
+        rec.p.y < pos.y + size.y && rec.p.z > pos.z - size.z && rec.p.z < pos.z + size.z) {
+      rec.n = scl(-1.0f, orient);
+      return true;
+    }
+    return false;
+  }
+  return false;
+}
+
+// Slab core of the build-defined box. inv = 1/d per axis,
+// lo/hi = the slab planes. Nearest entry / farthest exit, ties to the lower axis.
+struct Slab {
+  float tn, tf;
+  int an, af;
+};
+
+FR_HD float sel_min(float a, float b) { return a < b ? a : b; }
+FR_HD float sel_max(float a, float b) { return a < b ? b : a; }
+
+FR_HD Slab slab3(V3 lo, V3 hi, V3 o, V3 inv) {
+  const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
+  const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
+  const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
+  Slab s;
+  s.tn = sel_min(tx0, tx1);
+  s.an = 0;
+  const float ny = sel_min(ty0, ty1), nz = sel_min(tz0, tz1);
+  if (ny > s.tn) {
+    s.tn = ny;
+    s.an = 1;
+  }
+  if (nz > s.tn) {
+    s.tn = nz;
+    s.an = 2;
+  }
+  s.tf = sel_max(tx0, tx1);
+  s.af = 0;
+  const float fy = sel_max(ty0, ty1), fz = sel_max(tz0, tz1);
+  if (fy < s.tf) {
+    s.tf = fy;
+    s.af = 1;
+  }
+  if (fz < s.tf) {
+    s.tf = fz;
+    s.af = 2;
+  }
+  return s;
+}
+
+FR_HD float comp(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+// Outward normal of the face on axis k: entry face (near) opposes d, exit face follows it.
+FR_HD V3 axis_normal(int k, float s) {
+  return V3{k == 0 ? s : 0.0f, k == 1 ? s : 0.0f, k == 2 ? s : 0.0f};
+}
+
+// Axis-aligned box; `inv` = (1/d.x, 1/d.y, 1/d.z) (identical bits whether computed
+// per box or once per segment).
+FR_HD bool hit_aabb(V3 mn, V3 mx, V3 o, V3 d, V3 inv, float t_min, float t_max, HitRec& rec) {
+  const Slab s = slab3(mn, mx, o, inv);
+  if (s.tn < s.tf) {
+    if (s.tn > t_min && s.tn < t_max) {
+      rec.t = s.tn;
+      rec.p = add(o, scl(s.tn, d));
+      rec.n = axis_normal(s.an, comp(d, s.an) > 0.0f ? -1.0f : 1.0f);
+      return true;
+    }
+    if (s.tf > t_min && s.tf < t_max) {
+      rec.t = s.tf;
+      rec.p = add(o, scl(s.tf, d));
+      rec.n = axis_normal(s.af, comp(d, s.af) > 0.0f ? 1.0f : -1.0f);
+      return true;
+    }
+  }
+  return false;
+}
+
+// Oriented box: slab test in the box frame (rows ax, ay, az of world->local).
+FR_HD bool hit_obb(V3 c, V3 ax, V3 ay, V3 az, V3 h, V3 o, V3 d, float t_min, float t_max, HitRec& rec) {
+  const V3 oc = sub(o, c);
+  const V3 ol = V3{dot(ax, oc), dot(ay, oc), dot(az, oc)};
+  const V3 dl = V3{dot(ax, d), dot(ay, d), dot(az, d)};
+  const V3 inv = V3{1.0f / dl.x, 1.0f / dl.y, 1.0f / dl.z};
+  const V3 lo = V3{-h.x, -h.y, -h.z};
+  const Slab s = slab3(lo, h, ol, inv);
+  if (s.tn < s.tf) {
+    if (s.tn > t_min && s.tn < t_max) {
+      rec.t = s.tn;
+      rec.p = add(o, scl(s.tn, d));
+      const V3 axis = s.an == 0 ? ax : (s.an == 1 ? ay : az);
+      rec.n = scl(comp(dl, s.an) > 0.0f ? -1.0f : 1.0f, axis);
+      return true;
+    }
+    if (s.tf > t_min && s.tf < t_max) {
+      rec.t = s.tf;
+      rec.p = add(o, scl(s.tf, d));
+      const V3 axis = s.af == 0 ? ax : (s.af == 1 ? ay : az);
+      rec.n = scl(comp(dl, s.af) > 0.0f ? 1.0f : -1.0f, axis);
+      return true;
+    }
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// Scatter. Effective classes after the per-shape fallbacks (sphere.rs:56-69,
+// plane.rs:48-59): boxes follow the sphere's material table.
+// ---------------------------------------------------------------------------
+enum ScatterClass : uint32_t { SC_LAMBERT = 0, SC_METAL = 1, SC_DIELECTRIC = 2, SC_LIGHT = 3, SC_NONE = 4 };
+
+// sphere.rs:84-89 / 147-152, plane.rs:101-106: target = (p + n) + rus; dir = target - p
+FR_HD V3 scatter_lambert(V3 p, V3 n, Rng& r) {
+  const V3 target = add(add(p, n), random_in_unit_sphere(r));
+  return sub(target, p);
+}
+
+// sphere.rs:91-105, plane.rs:108-122: rus is drawn even when fuzz = 0
+FR_HD bool scatter_metal(V3 d, V3 p_unused, V3 n, float fuzz, Rng& r, V3& dir) {
+  (void)p_unused;
+  const V3 refl = reflect(unit(d), n);
+  dir = add(refl, scl(fuzz, random_in_unit_sphere(r)));
+  return dot(dir, n) > 0.0f;
+}
+
+// sphere.rs:107-145 (ref_idx 1.3; attenuation = colour, applied by the caller)
+FR_HD V3 scatter_dielectric(V3 d, V3 n, Rng& r) {
+  const float ref_idx = 1.3f;
+  const V3 reflected = reflect(d, n);
+  V3 outward;
+  float ni, cosine;
+  const float dn = dot(d, n);
+  if (dn > 0.0f) {
+    outward = sub(V3{0.0f, 0.0f, 0.0f}, n);
+    ni = ref_idx;
+    cosine = ref_idx * dot(d, n) / length(d);
+  } else {
+    outward = n;
+    ni = 1.0f / ref_idx;
+    cosine = -dot(d, n) / length(d);
+  }
+  // utility.rs:37-47
+  const V3 uv = unit(d);
+  const float dt = dot(uv, outward);
+  const float disc = 1.0f - ni * ni * (1.0f - dt * dt);
+  V3 refracted = V3{0.0f, 0.0f, 0.0f};
+  float reflect_prob;
+  if (disc > 0.0f) {
+    refracted = sub(scl(ni, sub(uv, scl(dt, outward))), scl(sqrtf(disc), outward));
+    reflect_prob = schlick(cosine, ref_idx);
+  } else {
+    reflect_prob = 1.0f;
+  }
+  return rng_f32(r) < reflect_prob ? reflected : refracted;
+}
+
+// tracer.rs:211-218
+FR_HD V3 sky(V3 d) {
+  const V3 ud = unit(d);
+  const float t = 0.5f * (ud.y + 1.0f);
+  return add(scl(1.0f - t, V3{1.0f, 1.0f, 1.0f}), scl(t, V3{0.5f, 0.7f, 1.0f}));
+}
+
+// tracer.rs:182-184: Rust `as u8` saturates (NaN -> 0) and truncates toward zero.
+FR_HD uint8_t to_u8(float c) {
+  const float s = sqrtf(c) * 255.0f;
+  if (!(s > 0.0f)) return 0;
+  if (s >= 255.0f) return 255;
+  return static_cast<uint8_t>(s);
+}
+
+}  // namespace fr

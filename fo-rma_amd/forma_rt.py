@@ -1,0 +1,461 @@
+"""Python host mirror of fo-rma's tracer API over libforma_rt's C ABI.
+
+Same names, argument meaning and failure behaviour as the reference's operator
+API in cpu_ray_tracer/tracer.rs (paths relative to the reference root):
+
+    create_model(width, height)          tracer.rs:19-28
+    update(model, keys, delta_time)      tracer.rs:30-55   (orbit camera + 1-spp frame)
+    save_image(model, sample, path)      tracer.rs:160-187 (sample spp, PNG)
+    TraceModel                           tracer.rs:12-17
+
+and the Hitable plugin API (shapes/hitable.rs:4-14): Sphere / Plane / Box objects
+with translate()/rotate(), flattened into the ordered primitive list the GPU
+kernel consumes. Rendering always runs the HIP kernel: if libforma_rt.so or a
+GPU is missing this module raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libforma_rt.so")
+SCENES_DIR = os.path.join(HERE, "scenes")
+
+FR_OK, FR_EARG, FR_EPARSE, FR_EHIP, FR_ENODEV, FR_ENOMEM = 0, -1, -2, -3, -4, -5
+FR_SPHERE, FR_PLANE, FR_AABB, FR_OBB, FR_STUB = 0, 1, 2, 3, 4
+FR_LAMBERTIAN, FR_METAL, FR_DIELECTRIC, FR_LIGHT = 0, 1, 2, 3
+FR_FLAG_WRITE_U8 = 1
+MAX_DEPTH = 50  # tracer.rs:10
+DEFAULT_SEED = 0x5EED
+
+
+class ForMaError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libforma_rt error {code}: {msg}")
+        self.code = code
+
+
+class FrPrim(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("material", C.c_uint32), ("color", C.c_float * 3), ("fuzz", C.c_float),
+                ("g", C.c_float * 16)]
+
+
+class FrCamera(C.Structure):
+    _fields_ = [(n, C.c_float * 3) for n in ("position", "lower_left", "horizontal", "vertical", "u", "v", "w")] + [
+        (n, C.c_float) for n in ("aspect", "lens_radius", "focus_dist", "radius", "rotation")]
+
+    def to_array(self):
+        vals = []
+        for n in ("position", "lower_left", "horizontal", "vertical", "u", "v", "w"):
+            vals.extend(getattr(self, n))
+        vals += [self.aspect, self.lens_radius, self.focus_dist, self.radius, self.rotation]
+        return np.asarray(vals, dtype=np.float32)
+
+
+class FrParams(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32), ("max_depth", C.c_uint32),
+                ("seed", C.c_uint64), ("strip_rows", C.c_uint32), ("shard_index", C.c_uint32),
+                ("shard_count", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class FrStats(C.Structure):
+    _fields_ = [("segments", C.c_uint64), ("hits", C.c_uint64), ("samples", C.c_uint64), ("prim_tests", C.c_uint64),
+                ("kernel_ms", C.c_double), ("total_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# Every symbol include/forma_rt.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "fr_last_error", "fr_abi_version", "fr_device_count",
+    "fr_scene_create", "fr_scene_builtin", "fr_scene_from_json", "fr_scene_free", "fr_scene_count",
+    "fr_scene_get_prims", "fr_scene_translate", "fr_scene_rotate",
+    "fr_camera_init", "fr_camera_look", "fr_camera_orbit", "fr_camera_translate", "fr_update_delta",
+    "fr_ctx_create", "fr_ctx_free", "fr_ctx_render", "fr_ctx_sync", "fr_ctx_download", "fr_ctx_device_buffers",
+    "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng",
+)
+
+_lib = None
+
+
+def _load_torch_runtime_first():
+    # If torch is importable, load it first so this library binds the same
+    # libamdhip64 (soname libamdhip64.so.7) as torch: one HIP runtime per process.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def lib():
+    """Load libforma_rt.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ForMaError(FR_ENODEV, f"{LIB_PATH} not built; run __graft_entry__.build() or make -C fo-rma_amd")
+    _load_torch_runtime_first()
+    L = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    vp = C.c_void_p
+    f3 = P(C.c_float)
+    L.fr_last_error.restype = C.c_char_p
+    L.fr_abi_version.restype = C.c_int
+    L.fr_device_count.argtypes = [P(C.c_int)]
+    L.fr_scene_create.argtypes = [P(FrPrim), C.c_uint32, P(vp)]
+    L.fr_scene_builtin.argtypes = [C.c_int, C.c_uint32, C.c_uint32, P(vp), P(FrCamera)]
+    L.fr_scene_from_json.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint32, P(vp), P(FrCamera)]
+    L.fr_scene_free.argtypes = [vp]
+    L.fr_scene_free.restype = None
+    L.fr_scene_count.argtypes = [vp]
+    L.fr_scene_count.restype = C.c_uint32
+    L.fr_scene_get_prims.argtypes = [vp, P(FrPrim), C.c_uint32]
+    L.fr_scene_translate.argtypes = [vp, C.c_uint32, f3]
+    L.fr_scene_rotate.argtypes = [vp, C.c_uint32, f3]
+    L.fr_camera_init.argtypes = [P(FrCamera), C.c_uint32, C.c_uint32]
+    L.fr_camera_look.argtypes = [P(FrCamera), f3, f3, f3, C.c_float, C.c_float, C.c_uint32, C.c_uint32]
+    L.fr_camera_orbit.argtypes = [P(FrCamera), f3]
+    L.fr_camera_translate.argtypes = [P(FrCamera), f3]
+    L.fr_update_delta.argtypes = [C.c_uint8, C.c_float, f3]
+    L.fr_ctx_create.argtypes = [C.c_int, vp, P(vp)]
+    L.fr_ctx_free.argtypes = [vp]
+    L.fr_ctx_free.restype = None
+    L.fr_ctx_render.argtypes = [vp, vp, P(FrCamera), P(FrParams)]
+    L.fr_ctx_sync.argtypes = [vp, P(FrStats)]
+    L.fr_ctx_download.argtypes = [vp, f3, P(C.c_uint8)]
+    L.fr_ctx_device_buffers.argtypes = [vp, P(vp), P(vp)]
+    L.fr_render_hip.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
+    L.fr_render_hip_multi.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
+    L.fr_selftest_ops.argtypes = [C.c_int, C.c_int, f3, f3, C.c_uint32, f3]
+    L.fr_selftest_rng.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != FR_OK:
+        raise ForMaError(rc, lib().fr_last_error().decode(errors="replace"))
+    return rc
+
+
+def _f3(v):
+    return (C.c_float * 3)(*[float(np.float32(x)) for x in v])
+
+
+def device_count():
+    n = C.c_int(0)
+    rc = lib().fr_device_count(C.byref(n))
+    return n.value if rc == FR_OK else 0
+
+
+# ---- Hitable plugin objects (shapes/hitable.rs:4-14) ------------------------
+
+class Hitable:
+    """Base of the tracer's shapes. translate/rotate are no-ops unless a shape
+    overrides them (hitable.rs:12-13)."""
+    kind = FR_STUB
+
+    def __init__(self, material=0, color=(0.0, 0.0, 0.0), fuzz=0.0):
+        self.material, self.color, self.fuzz = int(material), tuple(color), float(fuzz)
+
+    def geometry(self):
+        return ()
+
+    def translate(self, v):
+        pass
+
+    def rotate(self, v):
+        pass
+
+    def to_prim(self):
+        p = FrPrim()
+        p.kind, p.material, p.fuzz = self.kind, self.material, self.fuzz
+        for i in range(3):
+            p.color[i] = self.color[i]
+        for i, g in enumerate(self.geometry()):
+            p.g[i] = g
+        return p
+
+
+class Sphere(Hitable):
+    """shapes/sphere.rs: Sphere::new(center, radius, material, color, fuzz)"""
+    kind = FR_SPHERE
+
+    def __init__(self, center, radius, material, color, fuzz):
+        super().__init__(material, color, fuzz)
+        self.center, self.radius = tuple(center), float(radius)
+
+    def geometry(self):
+        return tuple(self.center) + (self.radius,)
+
+
+class Plane(Hitable):
+    """shapes/plane.rs: Plane::new(position, orientation, size, material, color, fuzz)"""
+    kind = FR_PLANE
+
+    def __init__(self, position, orientation, size, material, color, fuzz):
+        super().__init__(material, color, fuzz)
+        self.position, self.orientation, self.size = tuple(position), tuple(orientation), tuple(size)
+
+    def geometry(self):
+        return tuple(self.position) + tuple(self.orientation) + tuple(self.size)
+
+    def translate(self, v):  # plane.rs:62-64
+        self.position = tuple(v)
+
+    def rotate(self, v):  # plane.rs:66-68
+        self.orientation = tuple(v)
+
+
+class Box(Hitable):
+    """The build's axis-aligned box (FR_AABB), given by min/max corners."""
+    kind = FR_AABB
+
+    def __init__(self, mn, mx, material, color, fuzz):
+        super().__init__(material, color, fuzz)
+        self.mn, self.mx = tuple(mn), tuple(mx)
+
+    def geometry(self):
+        return tuple(self.mn) + tuple(self.mx)
+
+
+class Stub(Hitable):
+    """shapes/aabb.rs / rectangle.rs: never hit, never scatter."""
+    kind = FR_STUB
+
+
+# ---- scenes and cameras -----------------------------------------------------
+
+class Scene:
+    """An ordered primitive list on the host plus its resident device copies
+    (cpu_ray_tracer/scene.rs:4-7)."""
+
+    def __init__(self, handle, camera=None):
+        self._h = C.c_void_p(handle) if not isinstance(handle, C.c_void_p) else handle
+        self.camera = camera
+
+    @classmethod
+    def from_objects(cls, objects, camera=None):
+        arr = (FrPrim * max(1, len(objects)))(*[o.to_prim() for o in objects])
+        h = C.c_void_p()
+        check(lib().fr_scene_create(arr, len(objects), C.byref(h)))
+        return cls(h, camera)
+
+    @classmethod
+    def from_prims(cls, prims, camera=None):
+        """prims: sequence of FrPrim (or dicts with kind/material/color/fuzz/g)"""
+        arr = (FrPrim * max(1, len(prims)))()
+        for i, p in enumerate(prims):
+            if isinstance(p, FrPrim):
+                arr[i] = p
+            else:
+                arr[i].kind, arr[i].material, arr[i].fuzz = p["kind"], p["material"], float(p["fuzz"])
+                for k in range(3):
+                    arr[i].color[k] = float(p["color"][k])
+                for k in range(16):
+                    arr[i].g[k] = float(p["g"][k])
+        h = C.c_void_p()
+        check(lib().fr_scene_create(arr, len(prims), C.byref(h)))
+        return cls(h, camera)
+
+    @classmethod
+    def builtin(cls, which, width, height):
+        """0 get_simple_scene, 1 get_plane_scene, 2 get_objects (scenes.rs), 3 simple
+        scene in the interactive frontend's state. Camera = Camera::new(w, h)."""
+        h, cam = C.c_void_p(), FrCamera()
+        check(lib().fr_scene_builtin(which, width, height, C.byref(h), C.byref(cam)))
+        return cls(h, cam)
+
+    @classmethod
+    def from_json(cls, text, width, height):
+        if isinstance(text, str):
+            text = text.encode()
+        h, cam = C.c_void_p(), FrCamera()
+        check(lib().fr_scene_from_json(text, len(text), width, height, C.byref(h), C.byref(cam)))
+        return cls(h, cam)
+
+    @classmethod
+    def from_file(cls, path, width, height):
+        with open(path, "rb") as f:
+            return cls.from_json(f.read(), width, height)
+
+    def __len__(self):
+        return lib().fr_scene_count(self._h)
+
+    def prims(self):
+        n = len(self)
+        arr = (FrPrim * max(1, n))()
+        check(lib().fr_scene_get_prims(self._h, arr, n))
+        return [arr[i] for i in range(n)]
+
+    def translate(self, index, v):
+        check(lib().fr_scene_translate(self._h, index, _f3(v)))
+
+    def rotate(self, index, v):
+        check(lib().fr_scene_rotate(self._h, index, _f3(v)))
+
+    def close(self):
+        if self._h and self._h.value:
+            lib().fr_scene_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def camera_new(width, height):
+    cam = FrCamera()
+    check(lib().fr_camera_init(C.byref(cam), width, height))
+    return cam
+
+
+def camera_look(frm, at, vup, fov, aperture, width, height):
+    cam = FrCamera()
+    check(lib().fr_camera_look(C.byref(cam), _f3(frm), _f3(at), _f3(vup), float(fov), float(aperture), width,
+                               height))
+    return cam
+
+
+def camera_orbit(cam, delta):
+    check(lib().fr_camera_orbit(C.byref(cam), _f3(delta)))
+    return cam
+
+
+def camera_translate(cam, delta):
+    check(lib().fr_camera_translate(C.byref(cam), _f3(delta)))
+    return cam
+
+
+def scene_path(name):
+    """Path of a bundled scene file (the reference's scenes/*.json, re-serialised)."""
+    return os.path.join(SCENES_DIR, f"{name}.min.json")
+
+
+# ---- rendering ----------------------------------------------------------------
+
+def make_params(width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, shard_index=0, shard_count=1,
+                write_u8=True):
+    p = FrParams()
+    p.width, p.height, p.spp, p.max_depth, p.seed = width, height, spp, max_depth, seed
+    p.strip_rows, p.shard_index, p.shard_count = 8, shard_index, shard_count
+    p.flags = FR_FLAG_WRITE_U8 if write_u8 else 0
+    return p
+
+
+class RenderContext:
+    """One device, one HIP stream, resident output buffers (fr_ctx)."""
+
+    def __init__(self, device=0, stream=None):
+        self._h = C.c_void_p()
+        check(lib().fr_ctx_create(device, C.c_void_p(stream) if stream else None, C.byref(self._h)))
+        self.device = device
+
+    def render(self, scene, cam, params):
+        check(lib().fr_ctx_render(self._h, scene._h, C.byref(cam), C.byref(params)))
+
+    def sync(self):
+        st = FrStats()
+        check(lib().fr_ctx_sync(self._h, C.byref(st)))
+        return st.as_dict()
+
+    def download(self, width, height, mean=None, u8=None):
+        mean = np.full((height, width, 3), np.nan, dtype=np.float32) if mean is None else mean
+        u8 = np.zeros((height, width, 3), dtype=np.uint8) if u8 is None else u8
+        check(lib().fr_ctx_download(self._h, mean.ctypes.data_as(C.POINTER(C.c_float)),
+                                    u8.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return mean, u8
+
+    def close(self):
+        if self._h and self._h.value:
+            lib().fr_ctx_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render(scene, cam, width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, device=0, shard_index=0,
+           shard_count=1, n_gpus=1):
+    """Render on the GPU. Returns (mean[H,W,3] f32, u8[H,W,3], stats). Rows outside the
+    shard are NaN / 0. n_gpus > 1 row-shards the whole image across devices 0..n-1."""
+    mean = np.full((height, width, 3), np.nan, dtype=np.float32)
+    u8 = np.zeros((height, width, 3), dtype=np.uint8)
+    st = FrStats()
+    p = make_params(width, height, spp, max_depth, seed, shard_index, shard_count)
+    fm, fu = mean.ctypes.data_as(C.POINTER(C.c_float)), u8.ctypes.data_as(C.POINTER(C.c_uint8))
+    if n_gpus > 1:
+        check(lib().fr_render_hip_multi(scene._h, C.byref(cam), C.byref(p), n_gpus, fm, fu, C.byref(st)))
+    else:
+        check(lib().fr_render_hip(scene._h, C.byref(cam), C.byref(p), device, fm, fu, C.byref(st)))
+    return mean, u8, st.as_dict()
+
+
+# ---- tracer.rs operator API ---------------------------------------------------
+
+class TraceModel:
+    """tracer.rs:12-17 {scene, width, height, pixels}"""
+
+    def __init__(self, scene, width, height):
+        self.scene, self.width, self.height = scene, width, height
+        self.pixels = np.zeros(width * height * 3, dtype=np.uint8)
+        self.frame = 0
+        self.seed = DEFAULT_SEED
+        self.device = 0
+
+
+def create_model(width, height, scene=None):
+    """tracer.rs:19-28: Scene::new = get_simple_scene + Camera::new(w, h)."""
+    if scene is None:
+        scene = Scene.builtin(0, width, height)
+    elif scene.camera is None:
+        scene.camera = camera_new(width, height)
+    return TraceModel(scene, width, height)
+
+
+def update(model, keys, delta_time, max_depth=MAX_DEPTH):
+    """tracer.rs:30-55: key bitmask 00EQADWS -> camera.orbit(delta), then one 1-spp frame
+    into model.pixels. Each frame draws from its own RNG key."""
+    d = (C.c_float * 3)()
+    check(lib().fr_update_delta(int(keys) & 0xFF, float(delta_time), d))
+    camera_orbit(model.scene.camera, list(d))
+    seed = model.seed ^ (0x9E3779B97F4A7C15 * (model.frame + 1) & 0xFFFFFFFFFFFFFFFF)
+    model.frame += 1
+    _, u8, _ = render(model.scene, model.scene.camera, model.width, model.height, 1, max_depth, seed, model.device)
+    model.pixels = u8.reshape(-1)
+    return model.pixels
+
+
+def write_png(path, rgb8):
+    """Minimal RGB8 PNG writer (the reference uses the image crate, tracer.rs:186)."""
+    h, w, _ = rgb8.shape
+    raw = b"".join(b"\x00" + rgb8[y].tobytes() for y in range(h))
+
+    def chunk(tag, data):
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n")
+        f.write(chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0)))
+        f.write(chunk(b"IDAT", zlib.compress(raw, 6)))
+        f.write(chunk(b"IEND", b""))
+
+
+def save_image(model, sample, path="out/basic.png", max_depth=MAX_DEPTH):
+    """tracer.rs:160-187: `sample` spp per pixel, gamma 2, u8, PNG. Like the reference it
+    fails if the output directory is missing (tracer.rs:186 unwrap)."""
+    mean, u8, stats = render(model.scene, model.scene.camera, model.width, model.height, sample, max_depth,
+                             model.seed, model.device)
+    write_png(path, u8)
+    return mean, u8, stats

@@ -1,0 +1,194 @@
+/*
+ * forma_rt.h — C ABI of the MI355X-native path tracer that drops in for
+ * fo-rma's CPU ray tracer (zehreken/fo-rma, src/cpu_ray_tracer + src/shapes).
+ *
+ * Everything here is plain C: POD structs with explicit layout, opaque handles,
+ * integer error codes. No torch or HIP types appear in any signature (a HIP
+ * stream is passed as `void*`). A `#[repr(C)]` Rust mirror of this header is in
+ * INTEGRATION.md.
+ *
+ * Which reference interface each entry point replaces (paths relative to the
+ * reference root):
+ *
+ *   fr_prim / fr_scene_create ........ shapes/hitable.rs:4-14 (trait Hitable), the
+ *                                      Sphere/Plane/AABB/Rectangle constructors
+ *                                      (shapes/sphere.rs:75-83, plane.rs:48-66,
+ *                                      aabb.rs:36-44, rectangle.rs:36-44) and
+ *                                      cpu_ray_tracer/scene.rs:4-15 (Scene.objects)
+ *   fr_scene_builtin ................. cpu_ray_tracer/scenes.rs:6,41,110
+ *                                      (get_simple_scene / get_plane_scene / get_objects)
+ *   fr_scene_from_json ............... basics/scene_loader.rs:3-7 (construct_scene_from_json)
+ *                                      + basics/scene.rs:55-99 (mesh/material dispatch),
+ *                                      mapped to tracer primitives
+ *   fr_scene_translate / _rotate ..... shapes/hitable.rs:12-13, shapes/plane.rs:62-68
+ *   fr_camera_init ................... cpu_ray_tracer/camera.rs:24-60 (Camera::new)
+ *   fr_camera_look ................... camera.rs:24-60 generalised to a JSON camera
+ *   fr_camera_orbit .................. camera.rs:97-122 (Camera::orbit)
+ *   fr_camera_translate .............. camera.rs:74-95 (Camera::translate)
+ *   fr_update_delta .................. cpu_ray_tracer/tracer.rs:30-52 (update's key bitmask)
+ *   fr_ctx_render / fr_render_hip .... cpu_ray_tracer/tracer.rs:160-219 (save_image +
+ *                                      get_color) and tracer.rs:57-81 (render, 1 spp)
+ *   fr_render_hip_multi .............. tracer.rs:83-134 (render_mt row tiling), one
+ *                                      device per row shard instead of one thread
+ *
+ * Errors: 0 = ok, negative = FR_E*; the message is in fr_last_error() (thread-local).
+ * Threading: calls on distinct fr_scene / fr_ctx objects are re-entrant. A fr_ctx is
+ * bound to one device and one HIP stream and must not be used by two threads at once.
+ */
+#ifndef FORMA_RT_H
+#define FORMA_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FR_ABI_VERSION 1
+
+/* error codes */
+#define FR_OK 0
+#define FR_EARG (-1)   /* invalid argument */
+#define FR_EPARSE (-2) /* JSON syntax error or unsupported mesh */
+#define FR_EHIP (-3)   /* a HIP runtime call failed */
+#define FR_ENODEV (-4) /* no HIP device / requested device missing */
+#define FR_ENOMEM (-5) /* allocation failed */
+
+/* primitive kinds (one Hitable implementation each) */
+#define FR_SPHERE 0u /* shapes/sphere.rs */
+#define FR_PLANE 1u  /* shapes/plane.rs (bounded, world-axis extent) */
+#define FR_AABB 2u   /* build-defined axis-aligned box (JSON "cube" with a signed-permutation rotation) */
+#define FR_OBB 3u    /* build-defined oriented box (JSON "cube", any other rotation) */
+#define FR_STUB 4u   /* shapes/aabb.rs / rectangle.rs: hit() and scatter() always false */
+
+/* material ids as the reference stores them (u8 `material` field) */
+#define FR_LAMBERTIAN 0u /* sphere.rs:84-89, plane.rs:101-106 */
+#define FR_METAL 1u      /* sphere.rs:91-105, plane.rs:108-122 */
+#define FR_DIELECTRIC 2u /* sphere.rs:107-145 (spheres and boxes only) */
+#define FR_LIGHT 3u      /* sphere.rs:147-152 (no emission: attenuation 1) */
+
+/* flags for fr_params.flags */
+#define FR_FLAG_WRITE_U8 1u /* also write the u8 image (tracer.rs:177-184) */
+
+/*
+ * One primitive, in the order it is tested (list order decides ties, tracer.rs:195-200).
+ * Geometry `g` by kind:
+ *   FR_SPHERE : g[0..2] center, g[3] radius
+ *   FR_PLANE  : g[0..2] position, g[3..5] orientation, g[6..8] size (half extents per world axis)
+ *   FR_AABB   : g[0..2] min corner, g[3..5] max corner
+ *   FR_OBB    : g[0..2] center, g[3..5] local x axis, g[6..8] local y axis, g[9..11] local z axis
+ *               (unit rows of the world->local rotation), g[12..14] half extents
+ *   FR_STUB   : unused
+ * `material` is the raw reference id; unknown ids fall back as sphere.rs:68 / plane.rs:55 do.
+ */
+typedef struct fr_prim {
+  uint32_t kind;
+  uint32_t material;
+  float color[3];
+  float fuzz;
+  float g[16];
+} fr_prim;
+
+/* Mirrors the fields of cpu_ray_tracer::camera::Camera (camera.rs:8-21), f32 throughout. */
+typedef struct fr_camera {
+  float position[3];
+  float lower_left[3];
+  float horizontal[3];
+  float vertical[3];
+  float u[3];
+  float v[3];
+  float w[3];
+  float aspect;
+  float lens_radius;
+  float focus_dist; /* stored 2.0 by Camera::new, never used (camera.rs:56) */
+  float radius;     /* orbit radius, 5.0 (camera.rs:57) */
+  float rotation;   /* orbit angle, 0.0 (camera.rs:58) */
+} fr_camera;
+
+/*
+ * Render parameters. Rows are grouped into strips of `strip_rows` (must be 8) rows;
+ * strip k belongs to shard (k % shard_count). A shard renders only its own strips,
+ * so shards of one image are disjoint and stitch bit-exactly.
+ * RNG: one counter-based stream per (seed, global pixel index y*W+x, sample index).
+ */
+typedef struct fr_params {
+  uint32_t width, height;
+  uint32_t spp;       /* samples per pixel (save_image's `sample`) */
+  uint32_t max_depth; /* tracer.rs:10 MAX_DEPTH (reference default 50); 1..64 */
+  uint64_t seed;
+  uint32_t strip_rows;  /* must be 8 */
+  uint32_t shard_index; /* 0 <= shard_index < shard_count */
+  uint32_t shard_count; /* >= 1 */
+  uint32_t flags;       /* FR_FLAG_* */
+} fr_params;
+
+typedef struct fr_stats {
+  uint64_t segments;   /* get_color calls (ray segments traced) */
+  uint64_t hits;       /* segments whose closest-hit loop found an object */
+  uint64_t samples;    /* paths started = pixels * spp */
+  uint64_t prim_tests; /* segments * n_prims */
+  double kernel_ms;    /* HIP-event time of the trace kernel on its stream */
+  double total_ms;     /* host wall time of the call */
+} fr_stats;
+
+typedef struct fr_scene fr_scene; /* opaque: host primitive list + per-device copies */
+typedef struct fr_ctx fr_ctx;     /* opaque: one device, one stream, output buffers */
+
+/* ---- library ---- */
+const char* fr_last_error(void);
+int fr_abi_version(void);
+int fr_device_count(int* count);
+
+/* ---- scenes (host) ---- */
+int fr_scene_create(const fr_prim* prims, uint32_t n, fr_scene** out);
+int fr_scene_builtin(int which, uint32_t width, uint32_t height, fr_scene** out, fr_camera* cam_out);
+int fr_scene_from_json(const char* json_text, size_t len, uint32_t width, uint32_t height,
+                       fr_scene** out, fr_camera* cam_out);
+void fr_scene_free(fr_scene* scene);
+uint32_t fr_scene_count(const fr_scene* scene);
+int fr_scene_get_prims(const fr_scene* scene, fr_prim* out, uint32_t n);
+int fr_scene_translate(fr_scene* scene, uint32_t index, const float v[3]);
+int fr_scene_rotate(fr_scene* scene, uint32_t index, const float v[3]);
+
+/* ---- camera (host; tan/cos/sin are host-only) ---- */
+int fr_camera_init(fr_camera* cam, uint32_t width, uint32_t height);
+int fr_camera_look(fr_camera* cam, const float from[3], const float at[3], const float vup[3],
+                   float vfov_deg, float aperture, uint32_t width, uint32_t height);
+int fr_camera_orbit(fr_camera* cam, const float delta[3]);
+int fr_camera_translate(fr_camera* cam, const float delta[3]);
+int fr_update_delta(uint8_t keys, float delta_time, float delta_out[3]);
+
+/* ---- GPU render context ---- */
+int fr_ctx_create(int device, void* hip_stream /* NULL = own stream */, fr_ctx** out);
+void fr_ctx_free(fr_ctx* ctx);
+/* Enqueue one render of the shard described by params (async on the ctx stream).
+   The scene is uploaded to the ctx device on first use and stays resident. */
+int fr_ctx_render(fr_ctx* ctx, fr_scene* scene, const fr_camera* cam, const fr_params* params);
+/* Wait for the last render; fill counters and kernel time. */
+int fr_ctx_sync(fr_ctx* ctx, fr_stats* stats);
+/* Copy the shard's rows of the last render into full-image host buffers
+   (mean_rgb: W*H*3 f32, rgb8: W*H*3 u8; either may be NULL). Rows of other shards
+   are left untouched. */
+int fr_ctx_download(fr_ctx* ctx, float* mean_rgb, uint8_t* rgb8);
+/* Device pointers of the last render's full-image output buffers. */
+int fr_ctx_device_buffers(fr_ctx* ctx, float** d_mean_rgb, uint8_t** d_rgb8);
+
+/* ---- synchronous conveniences ---- */
+/* One shard on one device; writes the shard's rows into caller-owned host buffers. */
+int fr_render_hip(fr_scene* scene, const fr_camera* cam, const fr_params* params, int device,
+                  float* mean_rgb, uint8_t* rgb8, fr_stats* stats);
+/* The whole image row-sharded across devices 0..n_gpus-1 (one host thread + stream each). */
+int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* params, int n_gpus,
+                        float* mean_rgb, uint8_t* rgb8, fr_stats* stats);
+
+/* ---- diagnostics ---- */
+/* Run the device f32/RNG primitives on n inputs (op codes in DESIGN.md §7); used by the
+   parity tests to show the GPU arithmetic is bit-identical to the host's. */
+int fr_selftest_ops(int device, int op, const float* a, const float* b, uint32_t n, float* out);
+int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FORMA_RT_H */

@@ -1,0 +1,274 @@
+"""GPU parity: the gfx950 kernel (through the C ABI) against the oracle.
+
+Bar (BASELINE.json north star): per-channel |mean_gpu - mean_oracle| <= 1e-5.
+The kernel is built to match bit for bit, so these tests also require the u8
+image and the path counters (segments, hits) to be identical — counters catch a
+control-flow divergence before colour does. Full-size (1080p) configs are
+checked on a deterministic row subset that the oracle finishes in seconds.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle_py as O
+from oracle import scene_ref as S
+from tests.golden import make_golden as G
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5  # north-star tolerance, f32 means per channel
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def assert_parity(mean, u8, st, omean, ou8, ocnt, rows=None):
+    if rows is not None:
+        mean, u8, omean, ou8 = mean[rows], u8[rows], omean[rows], ou8[rows]
+    assert not np.isnan(mean).any()
+    err = float(np.max(np.abs(mean - omean))) if mean.size else 0.0
+    assert err <= TOL, f"max |d| = {err}"
+    assert np.array_equal(u8, ou8), f"u8 differs at {np.argwhere(u8 != ou8)[:5]}"
+    if ocnt is not None:
+        assert (st["segments"], st["hits"]) == (ocnt["segments"], ocnt["hits"])
+    return err
+
+
+# ---- device arithmetic --------------------------------------------------------
+
+def _edge_floats(rng, n):
+    special = np.array([0.0, -0.0, 1.0, -1.0, 1e-45, -1e-45, 1.17549435e-38, 3.4e38, -3.4e38, np.inf, -np.inf,
+                        np.nan, 0.5, 2.0, 1e-20, 1e20, 0.001, 1.3], dtype=np.float32)
+    bits = rng.integers(0, 2 ** 32, size=n, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    normal = rng.standard_normal(n).astype(np.float32) * np.float32(10.0)
+    return np.concatenate([special, bits, normal]).astype(np.float32)
+
+
+def _same_bits(a, b):
+    both_nan = np.isnan(a) & np.isnan(b)
+    return np.all(both_nan | (a.view(np.uint32) == b.view(np.uint32)))
+
+
+@pytest.mark.parametrize("op", ["add", "sub", "mul", "div", "sqrt", "recip"])
+def test_device_arithmetic_is_ieee_correctly_rounded(gpu, op):
+    import ctypes as C
+    rng = np.random.default_rng(1)
+    a = _edge_floats(rng, 20000)
+    b = np.roll(_edge_floats(rng, 20000), 7)
+    b = b[: a.size]
+    code = {"add": 0, "sub": 1, "mul": 2, "div": 3, "sqrt": 4, "recip": 8}[op]
+    out = np.empty_like(a)
+    fp = C.POINTER(C.c_float)
+    gpu.check(gpu.lib().fr_selftest_ops(0, code, a.ctypes.data_as(fp), b.ctypes.data_as(fp), a.size,
+                                        out.ctypes.data_as(fp)))
+    with np.errstate(all="ignore"):
+        want = {"add": a + b, "sub": a - b, "mul": a * b, "div": a / b, "sqrt": np.sqrt(a),
+                "recip": np.float32(1.0) / a}[op]
+    assert _same_bits(out, want.astype(np.float32))
+
+
+def test_device_schlick_unit_and_u8_match_oracle(gpu):
+    import ctypes as C
+    rng = np.random.default_rng(2)
+    c = rng.uniform(-0.2, 1.2, 4000).astype(np.float32)
+    ri = np.full_like(c, np.float32(1.3))
+    fp = C.POINTER(C.c_float)
+    out = np.empty_like(c)
+    gpu.check(gpu.lib().fr_selftest_ops(0, 5, c.ctypes.data_as(fp), ri.ctypes.data_as(fp), c.size,
+                                        out.ctypes.data_as(fp)))
+    want = np.array([O.vec3(12, (x, 1.3, 0))[0] for x in c[:500]], dtype=np.float32)
+    assert _same_bits(out[:500], want)
+    x, y = rng.standard_normal(4000).astype(np.float32), rng.standard_normal(4000).astype(np.float32)
+    gpu.check(gpu.lib().fr_selftest_ops(0, 7, x.ctypes.data_as(fp), y.ctypes.data_as(fp), x.size,
+                                        out.ctypes.data_as(fp)))
+    want = np.array([O.vec3(9, (a, b, 1.0))[0] for a, b in zip(x[:500], y[:500])], dtype=np.float32)
+    assert _same_bits(out[:500], want)
+    v = np.concatenate([np.linspace(-1, 2, 3000), [np.nan, np.inf, -np.inf, 1.0, 0.999999]]).astype(np.float32)
+    out = np.empty_like(v)
+    gpu.check(gpu.lib().fr_selftest_ops(0, 6, v.ctypes.data_as(fp), v.ctypes.data_as(fp), v.size,
+                                        out.ctypes.data_as(fp)))
+    with np.errstate(invalid="ignore"):
+        s = np.sqrt(v) * np.float32(255.0)
+    want = np.where(~(s > 0), 0, np.where(s >= 255, 255, np.trunc(np.nan_to_num(s)))).astype(np.float32)
+    assert np.array_equal(out, want)
+
+
+@pytest.mark.parametrize("seed,pixel,sample", [(0x5EED, 0, 0), (0x5EED, 2073599, 255), (7, 99, 1), (2 ** 63, 5, 9)])
+def test_device_rng_matches_oracle(gpu, seed, pixel, sample):
+    import ctypes as C
+    out = (C.c_uint32 * 200)()
+    gpu.check(gpu.lib().fr_selftest_rng(0, seed, pixel, sample, 200, out))
+    assert list(out) == list(O.rng_stream(seed, pixel, sample, 200))
+
+
+# ---- images -----------------------------------------------------------------------
+
+def _product_scene(fr, spec, w, h):
+    kind, name = spec.split(":")
+    if kind == "builtin":
+        return fr.Scene.builtin(int(name), w, h)
+    return fr.Scene.from_file(fr.scene_path(name), w, h)
+
+
+@pytest.mark.parametrize("name", sorted(G.CASES))
+def test_golden_cases(gpu, name):
+    spec, w, h, spp, depth, seed = G.CASES[name]
+    sc = _product_scene(gpu, spec, w, h)
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth, seed)
+    ref = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    cnt = {"segments": int(ref["counters"][0]), "hits": int(ref["counters"][1])}
+    assert_parity(mean, u8, st, ref["mean"], ref["u8"], cnt)
+    assert st["samples"] == int(ref["counters"][2])
+
+
+def random_scene(seed, n=12):
+    """Every primitive kind and material, placed around the default camera."""
+    r = np.random.default_rng(seed)
+    prims = []
+    for i in range(n):
+        kind = r.choice([S.SPHERE, S.SPHERE, S.PLANE, S.AABB, S.OBB, S.STUB])
+        mat = int(r.integers(0, 5))
+        col = r.uniform(0.1, 1.0, 3)
+        fuzz = float(r.uniform(0, 1))
+        c = r.uniform(-2, 2, 3) + np.array([0, 0, -2.5])
+        if kind == S.SPHERE:
+            prims.append(S.sphere(c, r.uniform(0.2, 1.2), mat, col, fuzz))
+        elif kind == S.PLANE:
+            o = np.zeros(3)
+            o[r.integers(0, 3)] = r.choice([-1.0, 1.0])
+            if r.uniform() < 0.3:
+                o = r.standard_normal(3)
+            prims.append(S.plane(c, o, r.uniform(0.5, 4, 3), mat, col, fuzz))
+        elif kind == S.AABB:
+            hsz = r.uniform(0.1, 1.0, 3)
+            prims.append(S.prim(S.AABB, mat, col, fuzz, list(c - hsz) + list(c + hsz)))
+        elif kind == S.OBB:
+            q = r.standard_normal(4)
+            q /= np.linalg.norm(q)
+            ax = S.quat_axes(*q)
+            prims.append(S.prim(S.OBB, mat, col, fuzz, list(c) + list(ax[0]) + list(ax[1]) + list(ax[2])
+                                + list(r.uniform(0.1, 1.0, 3))))
+        else:
+            prims.append(S.prim(S.STUB, mat, col, fuzz))
+    prims.append(S.sphere((0.0, -100.5, -1.0), 100.0, 0, (0.5, 0.5, 0.5), 0.0))
+    return prims
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_scenes_all_kinds_and_materials(gpu, seed):
+    w, h, spp, depth = 40, 24, 3, 8
+    prims = random_scene(seed)
+    sc = gpu.Scene.from_prims(prims)
+    cam = gpu.camera_new(w, h)
+    if seed % 2:
+        gpu.camera_orbit(cam, (0.4 * seed, 0.1, -2.0))
+    ocam = O.camera_new(w, h)
+    if seed % 2:
+        O.camera_orbit(ocam, (0.4 * seed, 0.1, -2.0))
+    mean, u8, st = gpu.render(sc, cam, w, h, spp, depth, seed=1000 + seed)
+    omean, ou8, ocnt, _ = O.render(prims, ocam, w, h, spp, depth, seed=1000 + seed, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+
+
+@pytest.mark.parametrize("shards", [2, 3, 8])
+def test_row_shards_stitch_bit_exactly(gpu, shards):
+    w, h, spp, depth = 100, 50, 4, 8  # H % 8 != 0: last strip is partial
+    sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
+    full, fu8, fst = gpu.render(sc, sc.camera, w, h, spp, depth)
+    mean = np.full_like(full, np.nan)
+    u8 = np.zeros_like(fu8)
+    seg = 0
+    for k in range(shards):
+        m, u, st = gpu.render(sc, sc.camera, w, h, spp, depth, shard_index=k, shard_count=shards)
+        rows = [y for y in range(h) if (y // 8) % shards == k]
+        assert np.isnan(m[[y for y in range(h) if y not in rows]]).all()  # other shards untouched
+        mean[rows], u8[rows] = m[rows], u[rows]
+        seg += st["segments"]
+    assert np.array_equal(mean.view(np.uint32), full.view(np.uint32)) and np.array_equal(u8, fu8)
+    assert seg == fst["segments"]
+
+
+def test_multi_device_api_with_one_device(gpu):
+    w, h = 48, 40
+    sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
+    a, au, _ = gpu.render(sc, sc.camera, w, h, 2, 8)
+    b, bu, _ = gpu.render(sc, sc.camera, w, h, 2, 8, n_gpus=1)
+    assert np.array_equal(a, b) and np.array_equal(au, bu)
+
+
+@pytest.mark.parametrize("case", ["spp1", "depth0", "depth64", "empty", "stubs", "tiny"])
+def test_edge_cases(gpu, case):
+    w, h, spp, depth, prims = 24, 16, 2, 8, S.BUILTIN[2]()
+    if case == "spp1":
+        spp = 1
+    elif case == "depth0":
+        depth = 0
+    elif case == "depth64":
+        depth, prims = 64, S.BUILTIN[3]()
+    elif case == "empty":
+        prims = []
+    elif case == "stubs":
+        prims = [S.prim(S.STUB)] * 3
+    elif case == "tiny":
+        w, h = 1, 1
+    sc = gpu.Scene.from_prims(prims)
+    cam, ocam = gpu.camera_new(w, h), O.camera_new(w, h)
+    mean, u8, st = gpu.render(sc, cam, w, h, spp, depth)
+    omean, ou8, ocnt, _ = O.render(prims, ocam, w, h, spp, depth)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+
+
+def test_context_reuse_and_scene_edits(gpu):
+    w, h = 32, 32
+    sc = gpu.Scene.builtin(0, w, h)
+    ctx = gpu.RenderContext(0)
+    ctx.render(sc, sc.camera, gpu.make_params(w, h, 2, 8))
+    ctx.sync()
+    a, _ = ctx.download(w, h)
+    sc.translate(0, (-1.0, 0.0, 0.0))
+    sc.rotate(0, (-1.0, 0.0, 0.0))  # the scene's device copy must be refreshed
+    ctx.render(sc, sc.camera, gpu.make_params(w, h, 2, 8))
+    st = ctx.sync()
+    b, bu = ctx.download(w, h)
+    omean, ou8, ocnt, _ = O.render(S.BUILTIN[3](), O.camera_new(w, h), w, h, 2, 8)
+    assert_parity(b, bu, st, omean, ou8, ocnt)
+    assert not np.array_equal(a, b)
+    ctx.close()
+
+
+def test_update_and_save_image_mirror(gpu, tmp_path):
+    w, h = 40, 30
+    m = gpu.create_model(w, h)
+    pix = gpu.update(m, 0b001000, 0.25)  # A key: orbit by +0.25 rad
+    assert pix.shape == (w * h * 3,) and pix.dtype == np.uint8
+    ocam = O.camera_orbit(O.camera_new(w, h), (0.25, 0.0, 0.0))
+    assert np.array_equal(m.scene.camera.to_array(), O.camera_to_array(ocam))
+    seed = m.seed ^ (0x9E3779B97F4A7C15 * 1 & 0xFFFFFFFFFFFFFFFF)
+    _, ou8, _, _ = O.render(S.BUILTIN[0](), ocam, w, h, 1, 50, seed=seed)
+    assert np.array_equal(pix.reshape(h, w, 3), ou8)
+    out = tmp_path / "basic.png"
+    mean, u8, st = gpu.save_image(m, 3, str(out))
+    assert out.read_bytes()[:8] == b"\x89PNG\r\n\x1a\n" and st["samples"] == w * h * 3
+
+
+# ---- full-size configurations (BASELINE.json configs), row subsets --------------
+
+def _rows(h, step):
+    return list(range(0, h, step))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("cfg", [("scene_08", 1920, 1080, 256, 8, 97), ("scene_01", 1920, 1080, 64, 8, 61)])
+def test_full_size_configs_on_row_subsets(gpu, cfg):
+    name, w, h, spp, depth, step = cfg
+    sc = gpu.Scene.from_file(gpu.scene_path(name), w, h)
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
+    assert st["samples"] == w * h * spp
+    prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path(name)).read())
+    cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
+    # the oracle renders every `step`-th row of the full image (row_step over shard 0 of 1)
+    omean, ou8, ocnt, n = O.render(prims, cam, w, h, spp, depth, row_step=step, threads=16)
+    rows = _rows(h, step)
+    assert n == len(rows)
+    assert_parity(mean, u8, st, omean, ou8, None, rows=rows)
+    # size-independent properties of the whole frame
+    assert np.isfinite(mean).all() and (mean >= 0).all() and (mean <= 1).all()
+    assert st["hits"] <= st["segments"] <= st["samples"] * (depth + 1)
