@@ -45,6 +45,7 @@ struct DeviceCopy {
   uint64_t version = 0;
   void* blob = nullptr;
   uint32_t n = 0;
+  bool has_plane = false;
   size_t off_kind = 0, off_g0 = 0, off_g1 = 0, off_g2 = 0, off_g3 = 0, off_mat = 0, off_cls = 0, off_att = 0;
 };
 
@@ -87,15 +88,31 @@ static uint32_t scatter_class(const fr_prim& p) {
 
 __device__ __forceinline__ V3 xyz(float4 a) { return V3{a.x, a.y, a.z}; }
 
+constexpr uint32_t kAttLds = 1024;  // attenuation table entries staged in LDS
+
+// HAS_PLANE: planes may leave the shared record's t/p stale (plane.rs:27-29), so
+// the last written t is tracked separately from the winner's.
+template <bool HAS_PLANE>
 __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KParams kp,
                                                         float* __restrict__ out_mean,
                                                         uint8_t* __restrict__ out_u8,
                                                         unsigned long long* __restrict__ counters) {
-  extern __shared__ uint32_t stack[];  // [max_depth][kBlock] primitive indices
+  // LDS: [attenuation rgb, n_att entries][stack: max_depth x kBlock primitive indices]
+  extern __shared__ uint32_t lds[];
+  const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
+  float* att_lds = reinterpret_cast<float*>(lds);
+  uint32_t* stack = lds + n_att * 3u;
   const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < n_att; i += kBlock) {
+    const float4 a = sc.att[i];
+    att_lds[3 * i + 0] = a.x;
+    att_lds[3 * i + 1] = a.y;
+    att_lds[3 * i + 2] = a.z;
+  }
+  __syncthreads();
+
   const uint32_t lane = tid & 63u;
   const uint32_t tile = blockIdx.x * (kBlock / 64u) + (tid >> 6);
-
   uint32_t x = 0, y = 0;
   bool valid = false;
   if (tile < kp.n_tiles) {
@@ -135,30 +152,34 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
       alive = true;
     }
     ++nseg;
-    // closest hit over the list in order (tracer.rs:190-200); one shared record
-    HitRec rec{0.0f, V3{0.0f, 0.0f, 0.0f}, V3{0.0f, 0.0f, 0.0f}};
-    float closest = FLT_MAX;
-    int best = -1;
+    // closest hit over the list in order (tracer.rs:190-200): only the accepted t of
+    // each test is needed here; the record is formed for the winner below.
     const V3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    const float a_dd = dot(d, d);
+    float closest = FLT_MAX, t_last = 0.0f;
+    int best = -1;
     for (uint32_t i = 0; i < sc.n; ++i) {
-      const uint32_t k = sc.kind[i];
-      bool h;
+      const uint32_t k = sc.kind[i];  // wave-uniform: scalar branch
+      float t = 0.0f;
+      bool h = false;
       if (k == FR_AABB) {
-        h = hit_aabb(xyz(sc.g0[i]), xyz(sc.g1[i]), o, d, inv, 0.001f, closest, rec);
+        h = slab_root(slab3(xyz(sc.g0[i]), xyz(sc.g1[i]), o, inv), 0.001f, closest, t);
       } else if (k == FR_SPHERE) {
         const float4 g = sc.g0[i];
-        h = hit_sphere(xyz(g), g.w, o, d, 0.001f, closest, rec);
+        h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, closest, t);
       } else if (k == FR_PLANE) {
-        h = hit_plane(xyz(sc.g0[i]), xyz(sc.g1[i]), xyz(sc.g2[i]), o, d, 0.001f, closest, rec);
+        const int r = plane_test(xyz(sc.g0[i]), xyz(sc.g1[i]), xyz(sc.g2[i]), o, d, 0.001f, closest, t);
+        if (r) t_last = t;
+        h = r == 2;
       } else if (k == FR_OBB) {
         const float4 a = sc.g0[i], b = sc.g1[i], c = sc.g2[i], e = sc.g3[i];
-        h = hit_obb(xyz(a), xyz(b), xyz(c), xyz(e), V3{a.w, b.w, c.w}, o, d, 0.001f, closest, rec);
-      } else {
-        h = false;  // shapes/aabb.rs, rectangle.rs stubs
+        const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
+        h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, closest, t);
       }
       if (h) {
-        closest = rec.t;
+        closest = t;
         best = static_cast<int>(i);
+        if (HAS_PLANE) t_last = t;
       }
     }
 
@@ -166,22 +187,40 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
     if (best >= 0) {
       ++nhit;
       if (depth < kp.max_depth) {
+        // the shared HitRecord: normal of the winner at its own t; p = point_at(last t written)
+        const V3 pw = add(o, scl(closest, d));
+        const uint32_t kb = sc.kind[best];
+        const float4 b0 = sc.g0[best], b1 = sc.g1[best];
+        V3 n;
+        if (kb == FR_AABB) {
+          n = slab_normal(slab3(xyz(b0), xyz(b1), o, inv), closest, d);
+        } else if (kb == FR_SPHERE) {
+          n = divs(sub(pw, xyz(b0)), b0.w);
+        } else if (kb == FR_PLANE) {
+          n = scl(-1.0f, xyz(b1));
+        } else {
+          const float4 b2 = sc.g2[best], b3 = sc.g3[best];
+          const ObbFrame f = obb_frame(xyz(b0), xyz(b1), xyz(b2), xyz(b3), o, d);
+          const Slab sl = slab3(V3{-b0.w, -b1.w, -b2.w}, V3{b0.w, b1.w, b2.w}, f.ol, f.inv);
+          n = obb_normal(xyz(b1), xyz(b2), xyz(b3), sl, closest, f.dl);
+        }
+        const V3 p = HAS_PLANE ? add(o, scl(t_last, d)) : pw;
         const uint32_t c = sc.cls[best];
         bool ok = true;
         V3 nd;
         if (c == SC_METAL) {
-          ok = scatter_metal(d, rec.p, rec.n, sc.mat[best].w, rng, nd);
+          ok = scatter_metal(d, p, n, sc.mat[best].w, rng, nd);
         } else if (c == SC_DIELECTRIC) {
-          nd = scatter_dielectric(d, rec.n, rng);
+          nd = scatter_dielectric(d, n, rng);
         } else if (c == SC_NONE) {
           ok = false;
         } else {
-          nd = scatter_lambert(rec.p, rec.n, rng);
+          nd = scatter_lambert(p, n, rng);
         }
         if (ok) {
           stack[depth * kBlock + tid] = static_cast<uint32_t>(best);
           ++depth;
-          o = rec.p;
+          o = p;
           d = nd;
           continue;
         }
@@ -192,7 +231,11 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
     }
     // attenuation * get_color(...) (tracer.rs:206-207), innermost first
     V3 col = term;
-    for (int j = static_cast<int>(depth) - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
+    for (int j = static_cast<int>(depth) - 1; j >= 0; --j) {
+      const uint32_t pi = stack[j * kBlock + tid];
+      const V3 a = n_att ? V3{att_lds[3 * pi], att_lds[3 * pi + 1], att_lds[3 * pi + 2]} : xyz(sc.att[pi]);
+      col = mul(a, col);
+    }
     sum = add(sum, col);
     alive = false;
     if (++s == kp.spp) todo = false;
@@ -336,6 +379,8 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   HIPCHK(hipMalloc(&c->blob, off));
   HIPCHK(hipMemcpy(c->blob, host.data(), off, hipMemcpyHostToDevice));
   c->n = n;
+  c->has_plane = false;
+  for (const fr_prim& p : s->prims) c->has_plane |= p.kind == FR_PLANE;
   c->version = s->version;
   *out = c;
   return FR_OK;
@@ -494,9 +539,15 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   if (kp.n_tiles) {
     const uint32_t blocks = (kp.n_tiles + 3u) / 4u;
-    const size_t lds = static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock * sizeof(uint32_t);
-    hipLaunchKernelGGL(trace_kernel, dim3(blocks), dim3(kBlock), lds, c->stream, ks, kc, kp, c->d_mean, c->d_u8,
-                       c->d_cnt);
+    const size_t n_att = dc->n <= kAttLds ? dc->n : 0u;
+    const size_t lds = n_att * 3 * sizeof(float) +
+                       static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock * sizeof(uint32_t);
+    if (dc->has_plane)
+      hipLaunchKernelGGL(trace_kernel<true>, dim3(blocks), dim3(kBlock), lds, c->stream, ks, kc, kp, c->d_mean,
+                         c->d_u8, c->d_cnt);
+    else
+      hipLaunchKernelGGL(trace_kernel<false>, dim3(blocks), dim3(kBlock), lds, c->stream, ks, kc, kp, c->d_mean,
+                         c->d_u8, c->d_cnt);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));

@@ -13,9 +13,9 @@
 //   random_in_unit_{circle,sphere} ... utility.rs:4-25 (rejection loops)
 //   Rng ............... replaces rand::thread_rng() (rand 0.9.2, Cargo.lock:2735) with a
 //                       counter-keyed xoshiro128** stream per (seed, pixel, sample)
-//   hit_sphere ........ shapes/sphere.rs:23-51
-//   hit_plane ......... shapes/plane.rs:24-44 (stale-record quirk kept)
-//   hit_aabb/hit_obb .. build-defined box, shaped like Sphere::hit
+//   sphere_root ....... shapes/sphere.rs:23-51
+//   plane_test ........ shapes/plane.rs:24-44 (stale-record quirk kept)
+//   slab3/slab_root ... build-defined box, shaped like Sphere::hit
 //   scatter_* ......... shapes/sphere.rs:84-152, shapes/plane.rs:101-122
 //   sky ............... cpu_ray_tracer/tracer.rs:211-218
 #pragma once
@@ -66,7 +66,7 @@ FR_HD float schlick(float cosine, float ref_idx) {
 
 // ---------------------------------------------------------------------------
 // RNG. One stream per (seed, pixel, sample): splitmix64 keys a xoshiro128**
-// state; f32 = (u32 >> 8) * 2^-24, the documented mapping of rand's f32 sampling.
+// state; f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits, as rand's f32 sampling).
 // ---------------------------------------------------------------------------
 struct Rng {
   uint32_t s0, s1, s2, s3;
@@ -102,13 +102,16 @@ FR_HD uint32_t rng_next(Rng& r) {  // xoshiro128** 1.1
   return result;
 }
 
-// u in [0, 2^24) scaled by 2^-24: exact, in [0, 1)
-FR_HD float rng_f32(Rng& r) { return static_cast<float>(rng_next(r) >> 8) * 5.9604644775390625e-08f; }
+// f32 in [0, 1): k = (u ^ 2^31) >> 8, r = k * 2^-24 (exact)
+FR_HD float rng_f32(Rng& r) {
+  return static_cast<float>((rng_next(r) ^ 0x80000000u) >> 8) * 5.9604644775390625e-08f;
+}
 
-// 2*r - 1 for r = k*2^-24 is exactly (k - 2^23) * 2^-23 (both sides exact in f32),
-// so one integer subtract replaces the reference's two float ops bit for bit.
+// 2*r - 1 for that r: (k - 2^23) * 2^-23 is exact in f32 and equals the arithmetic
+// shift (int32)u >> 8 scaled by 2^-23, so shift + convert + scale replace the
+// reference's 2*r - 1 bit for bit.
 FR_HD float rng_signed_unit(Rng& r) {
-  return static_cast<float>(static_cast<int32_t>(rng_next(r) >> 8) - 8388608) * 1.1920928955078125e-07f;
+  return static_cast<float>(static_cast<int32_t>(rng_next(r)) >> 8) * 1.1920928955078125e-07f;
 }
 
 // utility.rs:4-13: p = 2*(r1, r2, 0) - (1, 1, 0), retry while dot(p,p) >= 1
@@ -134,152 +137,124 @@ FR_HD V3 random_in_unit_sphere(Rng& r) {
 }
 
 // ---------------------------------------------------------------------------
-// Hit record / primitives
+// Primitives. The closest-hit loop (tracer.rs:190-200) only needs each test's
+// accepted t; the hit record's point and normal are formed once for the winner
+// (DESIGN.md §4.2 shows this equals the reference's shared-record updates).
 // ---------------------------------------------------------------------------
-struct HitRec {
-  float t;
-  V3 p;
-  V3 n;
-};
 
-// shapes/sphere.rs:23-51
-FR_HD bool hit_sphere(V3 c, float radius, V3 o, V3 d, float t_min, float t_max, HitRec& rec) {
+// shapes/sphere.rs:23-51 without the record writes; a = dot(d, d) (loop-invariant).
+// Both roots are formed unconditionally (no side effects) and the near one wins.
+FR_HD bool sphere_root(V3 c, float radius, V3 o, V3 d, float a, float t_min, float t_max, float& t) {
   const V3 oc = sub(o, c);
-  const float a = dot(d, d);
   const float b = dot(oc, d);
   const float cc = dot(oc, oc) - radius * radius;
   const float disc = b * b - a * cc;
   if (disc > 0.0f) {
     const float sq = sqrtf(disc);
     const float r1 = (-b - sq) / a;
-    if (r1 > t_min && r1 < t_max) {
-      rec.t = r1;
-      rec.p = add(o, scl(r1, d));
-      rec.n = divs(sub(rec.p, c), radius);
-      return true;
-    }
     const float r2 = (-b + sq) / a;
-    if (r2 > t_min && r2 < t_max) {
-      rec.t = r2;
-      rec.p = add(o, scl(r2, d));
-      rec.n = divs(sub(rec.p, c), radius);
-      return true;
-    }
+    const bool c1 = r1 > t_min && r1 < t_max;
+    const bool c2 = r2 > t_min && r2 < t_max;
+    t = c1 ? r1 : r2;
+    return c1 || c2;
   }
   return false;
 }
 
-// shapes/plane.rs:24-44 — denom is compared against the t-range; t and p are
-// written before the bounds test (a failed test leaves them stale); t may be < 0.
-FR_HD bool hit_plane(V3 pos, V3 orient, V3 size, V3 o, V3 d, float t_min, float t_max, HitRec& rec) {
+// shapes/plane.rs:24-44. denom is compared against the t-range; when it passes,
+// the record's t (and p = point_at(t)) are written before the bounds test, so a
+// failed test leaves them stale (returns 1); t may be negative. Returns 2 on a hit.
+FR_HD int plane_test(V3 pos, V3 orient, V3 size, V3 o, V3 d, float t_min, float t_max, float& t) {
   const float denom = dot(orient, d);
   if (denom > t_min && denom < t_max) {
-    const V3 ptr = sub(pos, o);
-    rec.t = dot(ptr, orient) / denom;
-    rec.p = add(o, scl(rec.t, d));
-    if (rec.p.x > pos.x - size.x && rec.p.x < pos.x + size.x && rec.p.y > pos.y - size.y &&
-        rec.p.y < pos.y + size.y && rec.p.z > pos.z - size.z && rec.p.z < pos.z + size.z) {
-      rec.n = scl(-1.0f, orient);
-      return true;
-    }
-    return false;
+    t = dot(sub(pos, o), orient) / denom;
+    const V3 p = add(o, scl(t, d));
+    const bool in = p.x > pos.x - size.x && p.x < pos.x + size.x && p.y > pos.y - size.y &&
+                    p.y < pos.y + size.y && p.z > pos.z - size.z && p.z < pos.z + size.z;
+    return in ? 2 : 1;
   }
-  return false;
+  return 0;
 }
 
-// Slab core of the build-defined box. inv = 1/d per axis,
-// lo/hi = the slab planes. Nearest entry / farthest exit, ties to the lower axis.
+// Build-defined box. Per axis k, with inv_k = 1/d_k:
+//   t0_k = (lo_k - o_k) * inv_k,  t1_k = (hi_k - o_k) * inv_k
+//   near_k = minNum(t0_k, t1_k),  far_k = maxNum(t0_k, t1_k)   (IEEE 754-2008, NaN-ignoring)
+//   tn = maxNum(maxNum(near_x, near_y), near_z),  tf = minNum(minNum(far_x, far_y), far_z)
+// Hit iff tn < tf and one root lies in (t_min, t_max); the near root wins (Sphere::hit's
+// two-root shape). The normal is the outward face normal of the first axis (x, y, z order)
+// whose near (far) value equals tn (tf): -sign(d_k) on entry, +sign(d_k) on exit,
+// with sign(0) counted negative. Zero signs never matter (t is only compared, never 0
+// when accepted), so the hardware min/max agree with the host's fminf/fmaxf.
+FR_HD float fmin_num(float a, float b) { return fminf(a, b); }
+FR_HD float fmax_num(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // v_max_f32 directly: the generic lowering re-canonicalises both operands first
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return fmaxf(a, b);
+#endif
+}
+
 struct Slab {
+  V3 t0, t1;  // slab distances per axis
   float tn, tf;
-  int an, af;
 };
 
-FR_HD float sel_min(float a, float b) { return a < b ? a : b; }
-FR_HD float sel_max(float a, float b) { return a < b ? b : a; }
-
 FR_HD Slab slab3(V3 lo, V3 hi, V3 o, V3 inv) {
-  const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
-  const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
-  const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
   Slab s;
-  s.tn = sel_min(tx0, tx1);
-  s.an = 0;
-  const float ny = sel_min(ty0, ty1), nz = sel_min(tz0, tz1);
-  if (ny > s.tn) {
-    s.tn = ny;
-    s.an = 1;
-  }
-  if (nz > s.tn) {
-    s.tn = nz;
-    s.an = 2;
-  }
-  s.tf = sel_max(tx0, tx1);
-  s.af = 0;
-  const float fy = sel_max(ty0, ty1), fz = sel_max(tz0, tz1);
-  if (fy < s.tf) {
-    s.tf = fy;
-    s.af = 1;
-  }
-  if (fz < s.tf) {
-    s.tf = fz;
-    s.af = 2;
-  }
+  s.t0 = V3{(lo.x - o.x) * inv.x, (lo.y - o.y) * inv.y, (lo.z - o.z) * inv.z};
+  s.t1 = V3{(hi.x - o.x) * inv.x, (hi.y - o.y) * inv.y, (hi.z - o.z) * inv.z};
+  s.tn = fmax_num(fmax_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y)), fmin_num(s.t0.z, s.t1.z));
+  s.tf = fmin_num(fmin_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y)), fmax_num(s.t0.z, s.t1.z));
   return s;
+}
+
+// Root selection: returns true and the accepted t if the box is hit in (t_min, t_max).
+FR_HD bool slab_root(const Slab& s, float t_min, float t_max, float& t) {
+  const bool c1 = s.tn > t_min && s.tn < t_max;
+  const bool c2 = s.tf > t_min && s.tf < t_max;
+  t = c1 ? s.tn : s.tf;
+  return s.tn < s.tf && (c1 || c2);
 }
 
 FR_HD float comp(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 
-// Outward normal of the face on axis k: entry face (near) opposes d, exit face follows it.
 FR_HD V3 axis_normal(int k, float s) {
   return V3{k == 0 ? s : 0.0f, k == 1 ? s : 0.0f, k == 2 ? s : 0.0f};
 }
 
-// Axis-aligned box; `inv` = (1/d.x, 1/d.y, 1/d.z) (identical bits whether computed
-// per box or once per segment).
-FR_HD bool hit_aabb(V3 mn, V3 mx, V3 o, V3 d, V3 inv, float t_min, float t_max, HitRec& rec) {
-  const Slab s = slab3(mn, mx, o, inv);
-  if (s.tn < s.tf) {
-    if (s.tn > t_min && s.tn < t_max) {
-      rec.t = s.tn;
-      rec.p = add(o, scl(s.tn, d));
-      rec.n = axis_normal(s.an, comp(d, s.an) > 0.0f ? -1.0f : 1.0f);
-      return true;
-    }
-    if (s.tf > t_min && s.tf < t_max) {
-      rec.t = s.tf;
-      rec.p = add(o, scl(s.tf, d));
-      rec.n = axis_normal(s.af, comp(d, s.af) > 0.0f ? 1.0f : -1.0f);
-      return true;
-    }
+// Outward normal of the accepted root t (t == tn: entry face, else exit face), in the
+// frame whose ray direction is dd.
+FR_HD V3 slab_normal(const Slab& s, float t, V3 dd) {
+  if (t == s.tn) {
+    const int k = fmin_num(s.t0.x, s.t1.x) == s.tn ? 0 : (fmin_num(s.t0.y, s.t1.y) == s.tn ? 1 : 2);
+    return axis_normal(k, comp(dd, k) > 0.0f ? -1.0f : 1.0f);
   }
-  return false;
+  const int k = fmax_num(s.t0.x, s.t1.x) == s.tf ? 0 : (fmax_num(s.t0.y, s.t1.y) == s.tf ? 1 : 2);
+  return axis_normal(k, comp(dd, k) > 0.0f ? 1.0f : -1.0f);
 }
 
-// Oriented box: slab test in the box frame (rows ax, ay, az of world->local).
-FR_HD bool hit_obb(V3 c, V3 ax, V3 ay, V3 az, V3 h, V3 o, V3 d, float t_min, float t_max, HitRec& rec) {
+// Oriented box: the same slab test in the box frame (rows ax, ay, az of world->local).
+struct ObbFrame {
+  V3 dl, inv, ol;
+};
+
+FR_HD ObbFrame obb_frame(V3 c, V3 ax, V3 ay, V3 az, V3 o, V3 d) {
+  ObbFrame f;
   const V3 oc = sub(o, c);
-  const V3 ol = V3{dot(ax, oc), dot(ay, oc), dot(az, oc)};
-  const V3 dl = V3{dot(ax, d), dot(ay, d), dot(az, d)};
-  const V3 inv = V3{1.0f / dl.x, 1.0f / dl.y, 1.0f / dl.z};
-  const V3 lo = V3{-h.x, -h.y, -h.z};
-  const Slab s = slab3(lo, h, ol, inv);
-  if (s.tn < s.tf) {
-    if (s.tn > t_min && s.tn < t_max) {
-      rec.t = s.tn;
-      rec.p = add(o, scl(s.tn, d));
-      const V3 axis = s.an == 0 ? ax : (s.an == 1 ? ay : az);
-      rec.n = scl(comp(dl, s.an) > 0.0f ? -1.0f : 1.0f, axis);
-      return true;
-    }
-    if (s.tf > t_min && s.tf < t_max) {
-      rec.t = s.tf;
-      rec.p = add(o, scl(s.tf, d));
-      const V3 axis = s.af == 0 ? ax : (s.af == 1 ? ay : az);
-      rec.n = scl(comp(dl, s.af) > 0.0f ? 1.0f : -1.0f, axis);
-      return true;
-    }
-  }
-  return false;
+  f.ol = V3{dot(ax, oc), dot(ay, oc), dot(az, oc)};
+  f.dl = V3{dot(ax, d), dot(ay, d), dot(az, d)};
+  f.inv = V3{1.0f / f.dl.x, 1.0f / f.dl.y, 1.0f / f.dl.z};
+  return f;
+}
+
+FR_HD V3 obb_normal(V3 ax, V3 ay, V3 az, const Slab& s, float t, V3 dl) {
+  const V3 nl = slab_normal(s, t, dl);  // one component is +-1
+  const float sg = nl.x + nl.y + nl.z;
+  const V3 axis = nl.x != 0.0f ? ax : (nl.y != 0.0f ? ay : az);
+  return scl(sg, axis);
 }
 
 // ---------------------------------------------------------------------------

@@ -75,7 +75,7 @@ struct ReflectRecord {
 
 // ---- the RNG that replaces rand::thread_rng() -------------------------------
 // splitmix64 (Steele, Lea & Flood 2014) keys xoshiro128** 1.1 (Blackman & Vigna
-// 2018) per (seed, pixel, sample); f32 = (u32 >> 8) * 2^-24 as rand's f32 sampling.
+// 2018) per (seed, pixel, sample); f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits).
 struct Rng {
   uint32_t s[4];
   static uint64_t splitmix(uint64_t& x) {
@@ -105,7 +105,7 @@ struct Rng {
     s[3] = rotl(s[3], 11);
     return result;
   }
-  float gen_f32() { return float(next_u32() >> 8) * (1.0f / 16777216.0f); }
+  float gen_f32() { return float((next_u32() ^ 0x80000000u) >> 8) * (1.0f / 16777216.0f); }
 };
 
 // ---- cpu_ray_tracer/utility.rs ---------------------------------------------
@@ -309,43 +309,48 @@ struct Stub : Hitable {
 
 // ---- build-defined box, restated from its written spec ------
 // Slabs per axis k: t0 = (lo_k - o_k) * (1/d_k), t1 = (hi_k - o_k) * (1/d_k);
-// near = max over axes of (t0<t1 ? t0 : t1), first axis wins ties; far = min over
-// axes of (t0<t1 ? t1 : t0). Hit iff near < far; then the near root if it is in
-// (t_min, t_max), else the far root — Sphere::hit's two-root shape. Outward face
-// normal: entry face = -sign(d_k) on the near axis, exit face = +sign(d_k) on the far
-// axis (sign(0) counts as negative). Scatter follows Sphere::scatter's material table.
+// near_k = fminf(t0, t1), far_k = fmaxf(t0, t1) (C99 fmin/fmax: NaN-ignoring);
+// tn = fmaxf(fmaxf(near_x, near_y), near_z), tf = fminf(fminf(far_x, far_y), far_z).
+// Hit iff tn < tf; then the near root if it is in (t_min, t_max), else the far root
+// (Sphere::hit's two-root shape). Normal: outward face of the first axis (x, y, z)
+// whose near value equals tn (entry, -sign(d_k)) or whose far value equals tf
+// (exit, +sign(d_k)); sign(0) counts as negative. Scatter: Sphere::scatter's table.
 struct BoxBase : Hitable {
   uint32_t material;
   Vec3 color;
   float fuzz;
   static float pick(Vec3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
-  static bool slabs(Vec3 lo, Vec3 hi, Vec3 o, Vec3 d, float& tn, int& an, float& tf, int& af) {
-    float t0[3], t1[3];
+  static bool slabs(Vec3 lo, Vec3 hi, Vec3 o, Vec3 d, float t_min, float t_max, float& t, Vec3& n_local) {
+    float t0[3], t1[3], nr[3], fr[3];
     for (int k = 0; k < 3; ++k) {
       const float inv = 1.0f / pick(d, k);
       t0[k] = (pick(lo, k) - pick(o, k)) * inv;
       t1[k] = (pick(hi, k) - pick(o, k)) * inv;
+      nr[k] = fminf(t0[k], t1[k]);
+      fr[k] = fmaxf(t0[k], t1[k]);
     }
-    tn = t0[0] < t1[0] ? t0[0] : t1[0];
-    an = 0;
-    tf = t0[0] < t1[0] ? t1[0] : t0[0];
-    af = 0;
-    for (int k = 1; k < 3; ++k) {
-      const float lo_k = t0[k] < t1[k] ? t0[k] : t1[k];
-      const float hi_k = t0[k] < t1[k] ? t1[k] : t0[k];
-      if (lo_k > tn) {
-        tn = lo_k;
-        an = k;
-      }
-      if (hi_k < tf) {
-        tf = hi_k;
-        af = k;
-      }
+    const float tn = fmaxf(fmaxf(nr[0], nr[1]), nr[2]);
+    const float tf = fminf(fminf(fr[0], fr[1]), fr[2]);
+    if (!(tn < tf)) return false;
+    int k;
+    float s;
+    if (tn > t_min && tn < t_max) {
+      t = tn;
+      k = nr[0] == tn ? 0 : (nr[1] == tn ? 1 : 2);
+      s = pick(d, k) > 0.0f ? -1.0f : 1.0f;
+    } else if (tf > t_min && tf < t_max) {
+      t = tf;
+      k = fr[0] == tf ? 0 : (fr[1] == tf ? 1 : 2);
+      s = pick(d, k) > 0.0f ? 1.0f : -1.0f;
+    } else {
+      return false;
     }
-    return tn < tf;
+    n_local = Vec3();
+    (k == 0 ? n_local.x : k == 1 ? n_local.y : n_local.z) = s;
+    return true;
   }
   bool scatter(Ray ray, HitRecord& rec, ReflectRecord& rr, Rng& rng) const override {
-    Sphere s;  // reuse the sphere's material code (sphere.rs:53-152)
+    Sphere s;  // the sphere's material code (sphere.rs:53-152)
     s.material = material;
     s.color = color;
     s.fuzz = fuzz;
@@ -356,29 +361,13 @@ struct BoxBase : Hitable {
 struct Aabb : BoxBase {
   Vec3 mn, mx;
   bool hit(Ray ray, float t_min, float t_max, HitRecord& rec) const override {
-    float tn, tf;
-    int an, af;
-    const Vec3 d = ray.direction();
-    if (!slabs(mn, mx, ray.origin(), d, tn, an, tf, af)) return false;
-    if (tn > t_min && tn < t_max) {
-      rec.t = tn;
-      rec.p = ray.point_at(tn);
-      Vec3 n;
-      const float s = pick(d, an) > 0.0f ? -1.0f : 1.0f;
-      (an == 0 ? n.x : an == 1 ? n.y : n.z) = s;
-      rec.normal = n;
-      return true;
-    }
-    if (tf > t_min && tf < t_max) {
-      rec.t = tf;
-      rec.p = ray.point_at(tf);
-      Vec3 n;
-      const float s = pick(d, af) > 0.0f ? 1.0f : -1.0f;
-      (af == 0 ? n.x : af == 1 ? n.y : n.z) = s;
-      rec.normal = n;
-      return true;
-    }
-    return false;
+    float t;
+    Vec3 n;
+    if (!slabs(mn, mx, ray.origin(), ray.direction(), t_min, t_max, t, n)) return false;
+    rec.t = t;
+    rec.p = ray.point_at(t);
+    rec.normal = n;
+    return true;
   }
 };
 
@@ -390,22 +379,15 @@ struct Obb : BoxBase {
     const Vec3 ol(Vec3::dot(ax[0], oc), Vec3::dot(ax[1], oc), Vec3::dot(ax[2], oc));
     const Vec3 dl(Vec3::dot(ax[0], d), Vec3::dot(ax[1], d), Vec3::dot(ax[2], d));
     const Vec3 lo(-half.x, -half.y, -half.z);
-    float tn, tf;
-    int an, af;
-    if (!slabs(lo, half, ol, dl, tn, an, tf, af)) return false;
-    if (tn > t_min && tn < t_max) {
-      rec.t = tn;
-      rec.p = ray.point_at(tn);
-      rec.normal = (pick(dl, an) > 0.0f ? -1.0f : 1.0f) * ax[an];
-      return true;
-    }
-    if (tf > t_min && tf < t_max) {
-      rec.t = tf;
-      rec.p = ray.point_at(tf);
-      rec.normal = (pick(dl, af) > 0.0f ? 1.0f : -1.0f) * ax[af];
-      return true;
-    }
-    return false;
+    float t;
+    Vec3 nl;
+    if (!slabs(lo, half, ol, dl, t_min, t_max, t, nl)) return false;
+    rec.t = t;
+    rec.p = ray.point_at(t);
+    // the local normal has one non-zero component s; world normal = s * that axis
+    const int k = nl.x != 0.0f ? 0 : (nl.y != 0.0f ? 1 : 2);
+    rec.normal = (nl.x + nl.y + nl.z) * ax[k];
+    return true;
   }
 };
 
