@@ -42,6 +42,27 @@ def shard_rows(height, shard, shards, strip=8):
     return [y for y in range(height) if (y // strip) % shards == shard]
 
 
+def gather_frame(mean_rgb, rank, world, height, strip=8):
+    """Stitch every rank's strips into rank 0's image (the optional final gather,
+    outside the timed region). `mean_rgb` is this rank's full-size [H, W, 3] buffer with
+    only its own strips valid. Returns the stitched frame on rank 0, None elsewhere."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return mean_rgb
+    mine = np.ascontiguousarray(mean_rgb[shard_rows(height, rank, world, strip)])
+    parts = [None] * world if rank == 0 else None
+    dist.gather_object(mine, parts, dst=0)
+    if rank != 0:
+        return None
+    out = np.empty_like(mean_rgb)
+    for r, part in enumerate(parts):
+        out[shard_rows(height, r, world, strip)] = part
+    return out
+
+
 def algorithmic_bytes(n_pixels, n_prims):
     """Compulsory HBM bytes of one trace launch: the scene read once
     (8 f32x4 / u32 records = 104 B per primitive) and the outputs written once
@@ -137,6 +158,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--verify", action="store_true", help="gather the frame on rank 0 and report a checksum")
     a = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -191,6 +213,13 @@ def main():
     flops_launch = algorithmic_flops(segs / len(stats), hits / len(stats), my_samples / len(stats), n_prims)
     tflops = flops_launch / (kernel_ms * 1e-3) / 1e12
 
+    checksum = None
+    if a.verify:
+        mean, _ = ctx.download(WIDTH, HEIGHT)
+        frame = gather_frame(mean, rank, world, HEIGHT)
+        if rank == 0:
+            import hashlib
+            checksum = hashlib.sha256(frame.tobytes()).hexdigest()[:16]
     if rank != 0:
         return
     value = total_samples / elapsed / 1e6
@@ -220,6 +249,8 @@ def main():
                           "unit": "TFLOP/s", "frac": round(tflops / FP32_PEAK_TFLOPS, 5),
                           "flops_per_launch": int(flops_launch), "note": "algorithmic lower bound, DESIGN.md §5"},
     }
+    if checksum:
+        out["frame_sha256_16"] = checksum
     if world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_budget)
     print(json.dumps(out), flush=True)

@@ -14,11 +14,27 @@
 // geometry arrives by scalar loads. Layout and rooflines: DESIGN.md §4-§5.
 #include <hip/hip_runtime.h>
 #include <float.h>
+#include <stdio.h>
 #include <string.h>
 #include <chrono>
 #include <thread>
 
 #include "internal.h"
+#ifdef FR_DIAG
+// rejection-loop trip counters (wave trips via first active lane, lane tries)
+__device__ unsigned long long g_fr_diag_lens[2];
+__device__ unsigned long long g_fr_diag_rus[2];
+#define FR_DIAG_TRY(arr)                                                           \
+  do {                                                                             \
+    const unsigned long long m_ = __ballot(1);                                     \
+    if ((threadIdx.x & 63u) == static_cast<uint32_t>(__ffsll(m_) - 1)) {             \
+      atomicAdd(&arr[0], 1ull);                                                    \
+      atomicAdd(&arr[1], static_cast<unsigned long long>(__popcll(m_)));           \
+    }                                                                              \
+  } while (0)
+#define FR_LENS_TRY() FR_DIAG_TRY(g_fr_diag_lens)
+#define FR_RUS_TRY() FR_DIAG_TRY(g_fr_diag_rus)
+#endif
 #include "rt_core.h"
 
 #define HIPCHK(call)                                                                      \
@@ -33,6 +49,10 @@ namespace fr {
 constexpr uint32_t kBlock = 256;      // 4 waves, one 8x8 pixel tile each
 constexpr uint32_t kStripRows = 8;    // rows per shard strip == tile height
 constexpr uint32_t kMaxDepth = 64;    // LDS stack bound (64 KB per workgroup)
+#ifndef FR_KREJ
+#define FR_KREJ 4  // rejection loop: lanes left to the next iteration (tuning only, results unchanged)
+#endif
+constexpr uint32_t kSmallDepth = 8;  // max_depth <= 8: attenuation-colour stack, unrolled unwind
 
 // ABI layout, mirrored by ctypes (forma_rt.py) and the Rust binding
 static_assert(sizeof(fr_prim) == 88, "fr_prim layout");
@@ -90,18 +110,57 @@ __device__ __forceinline__ V3 xyz(float4 a) { return V3{a.x, a.y, a.z}; }
 
 constexpr uint32_t kAttLds = 1024;  // attenuation table entries staged in LDS
 
+// FR_DIAG builds count, per phase, wave-level trips (one per SIMT pass of the wave)
+// and lane-level work, to measure SIMT efficiency. Never enabled in the product.
+#ifdef FR_DIAG
+enum { DG_ITER, DG_REGEN_W, DG_REGEN_L, DG_LENS_W, DG_LENS_L, DG_RUS_W, DG_RUS_L, DG_END_W, DG_END_L,
+       DG_UNW_W, DG_UNW_L, DG_HIT_W, DG_N };
+#define DIAG_WAVE(slot)                                                         \
+  do {                                                                          \
+    const unsigned long long m_ = __ballot(1);                                  \
+    if (lane == static_cast<uint32_t>(__ffsll(m_) - 1)) atomicAdd(&dg[slot], 1u); \
+  } while (0)
+#define DIAG_LANE(slot)                                                         \
+  do {                                                                          \
+    const unsigned long long m_ = __ballot(1);                                  \
+    if (lane == static_cast<uint32_t>(__ffsll(m_) - 1))                         \
+      atomicAdd(&dg[slot], static_cast<uint32_t>(__popcll(m_)));                \
+  } while (0)
+#else
+#define DIAG_WAVE(slot) do {} while (0)
+#define DIAG_LANE(slot) do {} while (0)
+#endif
+
 // HAS_PLANE: planes may leave the shared record's t/p stale (plane.rs:27-29), so
 // the last written t is tracked separately from the winner's.
-template <bool HAS_PLANE>
+__device__ __forceinline__ uint32_t lanes_set(bool b) { return static_cast<uint32_t>(__popcll(__ballot(b))); }
+
+// Per iteration of the lane loop (each lane owns one pixel and walks its samples in
+// order, so its f32 sum keeps the reference's sample order):
+//   1. one merged rejection loop serves both random_in_unit_circle (lens sample of a
+//      new camera ray, utility.rs:4-13) and random_in_unit_sphere (scatter,
+//      utility.rs:15-25): a circle try is a sphere try without the third draw, and
+//      dot(p,p) = (px*px + py*py) + 0 is the same value. Lanes of both kinds share the
+//      SIMT trips instead of running two loops. The loop stops once at most KREJ lanes
+//      of the wave still reject; those keep their RNG state and go on next iteration
+//      (their draws stay in stream order, so results do not depend on KREJ);
+//   2. closest hit + shading for lanes holding a ray;
+//   3. path end: unwind the attenuations, accumulate, seed the next sample.
+// MAXD > 0: max_depth <= MAXD is known at compile time and the stack holds the
+// attenuation colours themselves (12 B per level), unwound by an unrolled,
+// predicated sequence; MAXD == 0: any max_depth, the stack holds primitive indices.
+template <bool HAS_PLANE, int KREJ, int MAXD>
 __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KParams kp,
                                                         float* __restrict__ out_mean,
                                                         uint8_t* __restrict__ out_u8,
                                                         unsigned long long* __restrict__ counters) {
-  // LDS: [attenuation rgb, n_att entries][stack: max_depth x kBlock primitive indices]
+  // LDS: [attenuation rgb, n_att entries][stack: MAXD ? MAXD x 3 x kBlock f32 attenuations
+  //                                              : max_depth x kBlock primitive indices]
   extern __shared__ uint32_t lds[];
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
   float* att_lds = reinterpret_cast<float*>(lds);
   uint32_t* stack = lds + n_att * 3u;
+  float* astack = reinterpret_cast<float*>(stack);
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < n_att; i += kBlock) {
     const float4 a = sc.att[i];
@@ -109,6 +168,10 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
     att_lds[3 * i + 1] = a.y;
     att_lds[3 * i + 2] = a.z;
   }
+#ifdef FR_DIAG
+  __shared__ uint32_t dg[DG_N];
+  if (tid < DG_N) dg[tid] = 0;
+#endif
   __syncthreads();
 
   const uint32_t lane = tid & 63u;
@@ -129,116 +192,218 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
   const float fW = static_cast<float>(kp.W), fH = static_cast<float>(kp.H);
   const float fx = static_cast<float>(x), fy = static_cast<float>(kp.H - y);  // tracer.rs:171-172
 
-  V3 sum{0.0f, 0.0f, 0.0f};
-  V3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
-  Rng rng{0u, 0u, 0u, 0u};
-  uint32_t s = 0, depth = 0, nseg = 0, nhit = 0;
-  bool alive = false;
-  bool todo = valid && kp.spp > 0;
-
-  while (todo) {
-    if (!alive) {
-      // start sample s: jitter, then Camera::get_ray (camera.rs:62-72)
-      rng = rng_seed(kp.seed, pixel, s);
-      const float r0 = rng_f32(rng);
-      const float r1 = rng_f32(rng);
-      const float u = (fx + r0) / fW;
-      const float v = (fy + r1) / fH;
-      const V3 rd = scl(cam.lens, random_in_unit_circle(rng));
-      const V3 off = add(scl(rd.x, cu), scl(rd.y, cv));
-      o = add(cpos, off);
-      d = sub(sub(add(add(cllc, scl(u, chor)), scl(v, cver)), cpos), off);
-      depth = 0;
-      alive = true;
-    }
-    ++nseg;
-    // closest hit over the list in order (tracer.rs:190-200): only the accepted t of
-    // each test is needed here; the record is formed for the winner below.
-    const V3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-    const float a_dd = dot(d, d);
-    float closest = FLT_MAX, t_last = 0.0f;
-    int best = -1;
-    for (uint32_t i = 0; i < sc.n; ++i) {
-      const uint32_t k = sc.kind[i];  // wave-uniform: scalar branch
-      float t = 0.0f;
-      bool h = false;
-      if (k == FR_AABB) {
-        h = slab_root(slab3(xyz(sc.g0[i]), xyz(sc.g1[i]), o, inv), 0.001f, closest, t);
-      } else if (k == FR_SPHERE) {
-        const float4 g = sc.g0[i];
-        h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, closest, t);
-      } else if (k == FR_PLANE) {
-        const int r = plane_test(xyz(sc.g0[i]), xyz(sc.g1[i]), xyz(sc.g2[i]), o, d, 0.001f, closest, t);
-        if (r) t_last = t;
-        h = r == 2;
-      } else if (k == FR_OBB) {
-        const float4 a = sc.g0[i], b = sc.g1[i], c = sc.g2[i], e = sc.g3[i];
-        const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
-        h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, closest, t);
-      }
-      if (h) {
-        closest = t;
-        best = static_cast<int>(i);
-        if (HAS_PLANE) t_last = t;
-      }
-    }
-
-    V3 term;
-    if (best >= 0) {
-      ++nhit;
-      if (depth < kp.max_depth) {
-        // the shared HitRecord: normal of the winner at its own t; p = point_at(last t written)
-        const V3 pw = add(o, scl(closest, d));
-        const uint32_t kb = sc.kind[best];
-        const float4 b0 = sc.g0[best], b1 = sc.g1[best];
-        V3 n;
-        if (kb == FR_AABB) {
-          n = slab_normal(slab3(xyz(b0), xyz(b1), o, inv), closest, d);
-        } else if (kb == FR_SPHERE) {
-          n = divs(sub(pw, xyz(b0)), b0.w);
-        } else if (kb == FR_PLANE) {
-          n = scl(-1.0f, xyz(b1));
-        } else {
-          const float4 b2 = sc.g2[best], b3 = sc.g3[best];
-          const ObbFrame f = obb_frame(xyz(b0), xyz(b1), xyz(b2), xyz(b3), o, d);
-          const Slab sl = slab3(V3{-b0.w, -b1.w, -b2.w}, V3{b0.w, b1.w, b2.w}, f.ol, f.inv);
-          n = obb_normal(xyz(b1), xyz(b2), xyz(b3), sl, closest, f.dl);
-        }
-        const V3 p = HAS_PLANE ? add(o, scl(t_last, d)) : pw;
-        const uint32_t c = sc.cls[best];
-        bool ok = true;
-        V3 nd;
-        if (c == SC_METAL) {
-          ok = scatter_metal(d, p, n, sc.mat[best].w, rng, nd);
-        } else if (c == SC_DIELECTRIC) {
-          nd = scatter_dielectric(d, n, rng);
-        } else if (c == SC_NONE) {
-          ok = false;
-        } else {
-          nd = scatter_lambert(p, n, rng);
-        }
-        if (ok) {
-          stack[depth * kBlock + tid] = static_cast<uint32_t>(best);
-          ++depth;
-          o = p;
-          d = nd;
-          continue;
-        }
-      }
-      term = V3{0.0f, 0.0f, 0.0f};
+  enum : uint32_t { NEED_NONE = 0, NEED_LENS = 1, NEED_SPHERE = 2 };
+  uint32_t depth = 0;
+  auto att_of = [&](uint32_t pi) -> V3 {
+    return n_att ? V3{att_lds[3 * pi], att_lds[3 * pi + 1], att_lds[3 * pi + 2]} : xyz(sc.att[pi]);
+  };
+  // stack push at level `depth` of the scatter winner
+  auto push = [&](uint32_t pi) {
+    if (MAXD > 0) {
+      const V3 a = att_of(pi);
+      astack[(depth * 3 + 0) * kBlock + tid] = a.x;
+      astack[(depth * 3 + 1) * kBlock + tid] = a.y;
+      astack[(depth * 3 + 2) * kBlock + tid] = a.z;
     } else {
-      term = sky(d);
+      stack[depth * kBlock + tid] = pi;
     }
-    // attenuation * get_color(...) (tracer.rs:206-207), innermost first
-    V3 col = term;
-    for (int j = static_cast<int>(depth) - 1; j >= 0; --j) {
-      const uint32_t pi = stack[j * kBlock + tid];
-      const V3 a = n_att ? V3{att_lds[3 * pi], att_lds[3 * pi + 1], att_lds[3 * pi + 2]} : xyz(sc.att[pi]);
-      col = mul(a, col);
+  };
+  V3 sum{0.0f, 0.0f, 0.0f};
+  // the ray; while a lens sample is pending d.xy = (u, v); while a scatter sample is
+  // pending o = hit point and d = scatter base ((p + n), or reflect(unit(d), n) for metal)
+  V3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
+  V3 sn{0.0f, 0.0f, 0.0f};  // metal: normal
+  float sfuzz = 0.0f;
+  bool smetal = false;
+  uint32_t sbest = 0;
+  Rng rng{0u, 0u, 0u, 0u};
+  uint32_t s = 0, nseg = 0, nhit = 0;
+  bool active = valid && kp.spp > 0;
+  bool have_ray = false;
+  uint32_t need = NEED_NONE;
+  if (active) {
+    rng = rng_seed(kp.seed, pixel, 0u);  // the pixel's stream, drawn in sample order
+    const float r0 = rng_f32(rng);
+    const float r1 = rng_f32(rng);
+    d.x = (fx + r0) / fW;
+    d.y = (fy + r1) / fH;
+    need = NEED_LENS;
+  }
+
+  while (active) {
+    DIAG_WAVE(DG_ITER);
+    bool ended = false;
+    V3 term{0.0f, 0.0f, 0.0f};
+    if (need != NEED_NONE) {
+      // 1. merged rejection loop
+      float px = 0.0f, py = 0.0f, pz = 0.0f;
+      bool acc = false;
+      const bool sph = need == NEED_SPHERE;
+      do {
+        DIAG_WAVE(DG_LENS_W);
+        DIAG_LANE(DG_LENS_L);
+        if (!acc) {
+          px = rng_signed_unit(rng);
+          py = rng_signed_unit(rng);
+          pz = sph ? rng_signed_unit(rng) : 0.0f;
+          acc = !(px * px + py * py + pz * pz >= 1.0f);
+        }
+      } while (lanes_set(!acc) > static_cast<uint32_t>(KREJ));
+      if (acc) {
+        if (!sph) {
+          // Camera::get_ray (camera.rs:62-72)
+          const V3 rd = scl(cam.lens, V3{px, py, 0.0f});
+          const V3 off = add(scl(rd.x, cu), scl(rd.y, cv));
+          const float u = d.x, v = d.y;
+          o = add(cpos, off);
+          d = sub(sub(add(add(cllc, scl(u, chor)), scl(v, cver)), cpos), off);
+          depth = 0;
+          have_ray = true;
+        } else {
+          const V3 r{px, py, pz};
+          bool ok = true;
+          V3 dir;
+          if (smetal) {
+            dir = add(d, scl(sfuzz, r));  // reflected + fuzz * rus
+            ok = dot(dir, sn) > 0.0f;     // sphere.rs:104 / plane.rs:121
+          } else {
+            dir = sub(add(d, r), o);  // ((p + n) + rus) - p
+          }
+          if (ok) {
+            push(sbest);
+            ++depth;
+            d = dir;
+            have_ray = true;
+          } else {
+            ended = true;  // absorbed: get_color returns 0
+          }
+        }
+        need = NEED_NONE;
+      }
     }
-    sum = add(sum, col);
-    alive = false;
-    if (++s == kp.spp) todo = false;
+    if (have_ray) {
+      // 2. closest hit over the list in order (tracer.rs:190-200): only the accepted t
+      // of each test is needed here; the record is formed for the winner below.
+      ++nseg;
+      const V3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+      const float a_dd = dot(d, d);
+      float closest = FLT_MAX, t_last = 0.0f;
+      int best = -1;
+      for (uint32_t i = 0; i < sc.n; ++i) {
+        const uint32_t k = sc.kind[i];  // wave-uniform: scalar branch
+        float t = 0.0f;
+        bool h = false;
+        if (k == FR_AABB) {
+          h = slab_root(slab3(xyz(sc.g0[i]), xyz(sc.g1[i]), o, inv), 0.001f, closest, t);
+        } else if (k == FR_SPHERE) {
+          const float4 g = sc.g0[i];
+          h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, closest, t);
+        } else if (k == FR_PLANE) {
+          const int r = plane_test(xyz(sc.g0[i]), xyz(sc.g1[i]), xyz(sc.g2[i]), o, d, 0.001f, closest, t);
+          if (r) t_last = t;
+          h = r == 2;
+        } else if (k == FR_OBB) {
+          const float4 a = sc.g0[i], b = sc.g1[i], c = sc.g2[i], e = sc.g3[i];
+          const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
+          h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, closest, t);
+        }
+        if (h) {
+          closest = t;
+          best = static_cast<int>(i);
+          if (HAS_PLANE) t_last = t;
+        }
+      }
+      if (best < 0) {
+        term = sky(d);  // tracer.rs:211-218
+        ended = true;
+        have_ray = false;
+      } else {
+        DIAG_WAVE(DG_HIT_W);
+        ++nhit;
+        ended = true;  // unless a scatter continues the path
+        have_ray = false;
+        if (depth < kp.max_depth) {
+          // the shared HitRecord: normal of the winner at its own t; p = point_at(last t written)
+          const V3 pw = add(o, scl(closest, d));
+          const uint32_t kb = sc.kind[best];
+          const float4 b0 = sc.g0[best], b1 = sc.g1[best];
+          V3 n;
+          if (kb == FR_AABB) {
+            n = slab_normal(slab3(xyz(b0), xyz(b1), o, inv), closest, d);
+          } else if (kb == FR_SPHERE) {
+            n = divs(sub(pw, xyz(b0)), b0.w);
+          } else if (kb == FR_PLANE) {
+            n = scl(-1.0f, xyz(b1));
+          } else {
+            const float4 b2 = sc.g2[best], b3 = sc.g3[best];
+            const ObbFrame f = obb_frame(xyz(b0), xyz(b1), xyz(b2), xyz(b3), o, d);
+            const Slab sl = slab3(V3{-b0.w, -b1.w, -b2.w}, V3{b0.w, b1.w, b2.w}, f.ol, f.inv);
+            n = obb_normal(xyz(b1), xyz(b2), xyz(b3), sl, closest, f.dl);
+          }
+          const V3 p = HAS_PLANE ? add(o, scl(t_last, d)) : pw;
+          const uint32_t c = sc.cls[best];
+          if (c == SC_DIELECTRIC) {
+            // one draw, no rejection loop (sphere.rs:107-145)
+            const V3 nd = scatter_dielectric(d, n, rng);
+            push(static_cast<uint32_t>(best));
+            ++depth;
+            o = p;
+            d = nd;
+            have_ray = true;
+            ended = false;
+          } else if (c != SC_NONE) {
+            // lambertian / light: target = (p + n) + rus; metal: reflect(unit(d), n) + fuzz * rus
+            sbest = static_cast<uint32_t>(best);
+            smetal = c == SC_METAL;
+            if (smetal) {
+              sfuzz = sc.mat[best].w;
+              sn = n;
+              d = reflect(unit(d), n);
+            } else {
+              d = add(p, n);
+            }
+            o = p;
+            need = NEED_SPHERE;
+            ended = false;
+          }
+        }
+      }
+    }
+    if (ended) {
+      // 3. attenuation * get_color(...) (tracer.rs:206-207), innermost first
+      DIAG_WAVE(DG_END_W);
+      DIAG_LANE(DG_END_L);
+      V3 col = term;
+      if (MAXD > 0) {
+#pragma unroll
+        for (int j = MAXD - 1; j >= 0; --j) {
+          if (j < static_cast<int>(depth)) {
+            DIAG_WAVE(DG_UNW_W);
+            DIAG_LANE(DG_UNW_L);
+            const V3 a{astack[(j * 3 + 0) * kBlock + tid], astack[(j * 3 + 1) * kBlock + tid],
+                       astack[(j * 3 + 2) * kBlock + tid]};
+            col = mul(a, col);
+          }
+        }
+      } else {
+        for (int j = static_cast<int>(depth) - 1; j >= 0; --j) {
+          DIAG_WAVE(DG_UNW_W);
+          DIAG_LANE(DG_UNW_L);
+          col = mul(att_of(stack[j * kBlock + tid]), col);
+        }
+      }
+      sum = add(sum, col);
+      if (++s == kp.spp) {
+        active = false;
+      } else {
+        // next sample: jitter (tracer.rs:171-172); the lens sample follows in step 1
+        const float r0 = rng_f32(rng);
+        const float r1 = rng_f32(rng);
+        d.x = (fx + r0) / fW;
+        d.y = (fy + r1) / fH;
+        need = NEED_LENS;
+      }
+    }
   }
 
   if (valid) {
@@ -263,6 +428,10 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
     atomicAdd(&counters[0], a);
     atomicAdd(&counters[1], b);
   }
+#ifdef FR_DIAG
+  __syncthreads();
+  if (tid < DG_N) atomicAdd(&counters[4 + tid], static_cast<unsigned long long>(dg[tid]));
+#endif
 }
 
 // ---- diagnostics kernels ---------------------------------------------------
@@ -465,7 +634,7 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
     c->own_stream = true;
   }
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      hipMalloc(&c->d_cnt, 4 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc(&c->d_cnt, 32 * sizeof(unsigned long long)) != hipSuccess) {
     fr_ctx_free(c);
     return set_error(FR_EHIP, "fr_ctx_create: event/counter allocation failed");
   }
@@ -535,19 +704,35 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
       strips > p->shard_index ? (strips - p->shard_index + p->shard_count - 1) / p->shard_count : 0u;
   kp.n_tiles = my_strips * kp.tiles_per_row;
   c->t0 = std::chrono::steady_clock::now();
-  HIPCHK(hipMemsetAsync(c->d_cnt, 0, 4 * sizeof(unsigned long long), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_cnt, 0, 32 * sizeof(unsigned long long), c->stream));
+#ifdef FR_DIAG
+  {
+    const unsigned long long z[2] = {0, 0};
+    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fr_diag_lens), z, sizeof(z), 0, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fr_diag_rus), z, sizeof(z), 0, hipMemcpyHostToDevice, c->stream));
+  }
+#endif
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   if (kp.n_tiles) {
     const uint32_t blocks = (kp.n_tiles + 3u) / 4u;
     const size_t n_att = dc->n <= kAttLds ? dc->n : 0u;
-    const size_t lds = n_att * 3 * sizeof(float) +
-                       static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock * sizeof(uint32_t);
-    if (dc->has_plane)
-      hipLaunchKernelGGL(trace_kernel<true>, dim3(blocks), dim3(kBlock), lds, c->stream, ks, kc, kp, c->d_mean,
+    const bool small_depth = p->max_depth <= kSmallDepth;
+    const size_t stack_bytes = small_depth ? kSmallDepth * 3 * kBlock * sizeof(float)
+                                           : static_cast<size_t>(p->max_depth) * kBlock * sizeof(uint32_t);
+    const size_t lds = n_att * 3 * sizeof(float) + stack_bytes;
+    const dim3 g(blocks), b(kBlock);
+    if (dc->has_plane && small_depth)
+      hipLaunchKernelGGL((trace_kernel<true, FR_KREJ, kSmallDepth>), g, b, lds, c->stream, ks, kc, kp, c->d_mean,
+                         c->d_u8, c->d_cnt);
+    else if (dc->has_plane)
+      hipLaunchKernelGGL((trace_kernel<true, FR_KREJ, 0>), g, b, lds, c->stream, ks, kc, kp, c->d_mean, c->d_u8,
+                         c->d_cnt);
+    else if (small_depth)
+      hipLaunchKernelGGL((trace_kernel<false, FR_KREJ, kSmallDepth>), g, b, lds, c->stream, ks, kc, kp, c->d_mean,
                          c->d_u8, c->d_cnt);
     else
-      hipLaunchKernelGGL(trace_kernel<false>, dim3(blocks), dim3(kBlock), lds, c->stream, ks, kc, kp, c->d_mean,
-                         c->d_u8, c->d_cnt);
+      hipLaunchKernelGGL((trace_kernel<false, FR_KREJ, 0>), g, b, lds, c->stream, ks, kc, kp, c->d_mean, c->d_u8,
+                         c->d_cnt);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));
@@ -563,8 +748,21 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
   HIPCHK(hipStreamSynchronize(c->stream));
   if (!c->pending) return set_error(FR_EARG, "fr_ctx_sync: nothing rendered");
   if (st) {
-    unsigned long long cnt[4] = {0, 0, 0, 0};
+    unsigned long long cnt[32] = {};
     HIPCHK(hipMemcpy(cnt, c->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
+#ifdef FR_DIAG
+    unsigned long long dl[2], dr[2];
+    HIPCHK(hipMemcpyFromSymbol(dl, HIP_SYMBOL(g_fr_diag_lens), sizeof(dl)));
+    HIPCHK(hipMemcpyFromSymbol(dr, HIP_SYMBOL(g_fr_diag_rus), sizeof(dr)));
+    fprintf(stderr,
+            "FR_DIAG {\"iter_w\": %llu, \"regen_w\": %llu, \"regen_l\": %llu, \"hit_w\": %llu, \"end_w\": %llu, "
+            "\"end_l\": %llu, \"unwind_w\": %llu, \"unwind_l\": %llu, \"lens_w\": %llu, \"lens_l\": %llu, "
+            "\"rus_w\": %llu, \"rus_l\": %llu, \"merged_w\": %llu, \"merged_l\": %llu, \"segments\": %llu, "
+            "\"hits\": %llu}\n",
+            cnt[4 + DG_ITER], cnt[4 + DG_REGEN_W], cnt[4 + DG_REGEN_L], cnt[4 + DG_HIT_W], cnt[4 + DG_END_W],
+            cnt[4 + DG_END_L], cnt[4 + DG_UNW_W], cnt[4 + DG_UNW_L], dl[0], dl[1], dr[0], dr[1], cnt[4 + DG_LENS_W],
+            cnt[4 + DG_LENS_L], cnt[0], cnt[1]);
+#endif
     float ms = 0.0f;
     HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     const fr_params& p = c->last;

@@ -65,8 +65,12 @@ FR_HD float schlick(float cosine, float ref_idx) {
 }
 
 // ---------------------------------------------------------------------------
-// RNG. One stream per (seed, pixel, sample): splitmix64 keys a xoshiro128**
-// state; f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits, as rand's f32 sampling).
+// RNG. One stream per (seed, pixel): splitmix64 keys a xoshiro128+ 1.0 state
+// (Blackman & Vigna's generator for floating-point output: only the upper bits are
+// used); the pixel's samples draw from it in sample order, as the reference's
+// save_image draws every sample from one sequential stream (tracer.rs:164-175).
+// f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits). `stream` selects independent
+// streams of one pixel (0 for rendering; the self-tests use others).
 // ---------------------------------------------------------------------------
 struct Rng {
   uint32_t s0, s1, s2, s3;
@@ -80,8 +84,8 @@ FR_HD uint64_t splitmix64_next(uint64_t& x) {
   return z ^ (z >> 31);
 }
 
-FR_HD Rng rng_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {
-  uint64_t x = seed ^ ((static_cast<uint64_t>(pixel) << 32) | static_cast<uint64_t>(sample));
+FR_HD Rng rng_seed(uint64_t seed, uint32_t pixel, uint32_t stream) {
+  uint64_t x = seed ^ ((static_cast<uint64_t>(pixel) << 32) | static_cast<uint64_t>(stream));
   uint64_t a = splitmix64_next(x);
   uint64_t b = splitmix64_next(x);
   return Rng{static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
@@ -90,8 +94,8 @@ FR_HD Rng rng_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {
 
 FR_HD uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
 
-FR_HD uint32_t rng_next(Rng& r) {  // xoshiro128** 1.1
-  const uint32_t result = rotl32(r.s1 * 5u, 7) * 9u;
+FR_HD uint32_t rng_next(Rng& r) {  // xoshiro128+ 1.0
+  const uint32_t result = r.s0 + r.s3;
   const uint32_t t = r.s1 << 9;
   r.s2 ^= r.s0;
   r.s3 ^= r.s1;
@@ -115,9 +119,14 @@ FR_HD float rng_signed_unit(Rng& r) {
 }
 
 // utility.rs:4-13: p = 2*(r1, r2, 0) - (1, 1, 0), retry while dot(p,p) >= 1
+#ifndef FR_LENS_TRY
+#define FR_LENS_TRY()
+#define FR_RUS_TRY()
+#endif
 FR_HD V3 random_in_unit_circle(Rng& r) {
   float px, py;
   do {
+    FR_LENS_TRY();
     px = rng_signed_unit(r);
     py = rng_signed_unit(r);
     // dot(p,p) = (px*px + py*py) + 0*0; adding +0 to a sum of squares is exact
@@ -129,6 +138,7 @@ FR_HD V3 random_in_unit_circle(Rng& r) {
 FR_HD V3 random_in_unit_sphere(Rng& r) {
   float px, py, pz;
   do {
+    FR_RUS_TRY();
     px = rng_signed_unit(r);
     py = rng_signed_unit(r);
     pz = rng_signed_unit(r);
@@ -204,8 +214,18 @@ struct Slab {
 
 FR_HD Slab slab3(V3 lo, V3 hi, V3 o, V3 inv) {
   Slab s;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // same IEEE ops, two lanes per instruction (v_pk_add_f32 / v_pk_mul_f32)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 oxy = {o.x, o.y}, ixy = {inv.x, inv.y};
+  const f2 a = (f2{lo.x, lo.y} - oxy) * ixy;
+  const f2 b = (f2{hi.x, hi.y} - oxy) * ixy;
+  s.t0 = V3{a.x, a.y, (lo.z - o.z) * inv.z};
+  s.t1 = V3{b.x, b.y, (hi.z - o.z) * inv.z};
+#else
   s.t0 = V3{(lo.x - o.x) * inv.x, (lo.y - o.y) * inv.y, (lo.z - o.z) * inv.z};
   s.t1 = V3{(hi.x - o.x) * inv.x, (hi.y - o.y) * inv.y, (hi.z - o.z) * inv.z};
+#endif
   s.tn = fmax_num(fmax_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y)), fmin_num(s.t0.z, s.t1.z));
   s.tf = fmin_num(fmin_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y)), fmax_num(s.t0.z, s.t1.z));
   return s;

@@ -74,8 +74,10 @@ struct ReflectRecord {
 };
 
 // ---- the RNG that replaces rand::thread_rng() -------------------------------
-// splitmix64 (Steele, Lea & Flood 2014) keys xoshiro128** 1.1 (Blackman & Vigna
-// 2018) per (seed, pixel, sample); f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits).
+// splitmix64 (Steele, Lea & Flood 2014) keys xoshiro128+ 1.0 (Blackman & Vigna
+// 2018) per (seed, pixel, stream); rendering uses stream 0 of each pixel and draws
+// the pixel's samples from it in order, like save_image's one sequential ThreadRng
+// (tracer.rs:164-175); f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits).
 struct Rng {
   uint32_t s[4];
   static uint64_t splitmix(uint64_t& x) {
@@ -95,7 +97,7 @@ struct Rng {
   }
   static uint32_t rotl(uint32_t v, int k) { return (v << k) | (v >> (32 - k)); }
   uint32_t next_u32() {
-    uint32_t result = rotl(s[1] * 5u, 7) * 9u;
+    uint32_t result = s[0] + s[3];
     uint32_t t = s[1] << 9;
     s[2] ^= s[0];
     s[3] ^= s[1];
@@ -705,8 +707,8 @@ int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, ui
       for (uint32_t x = 0; x < width; ++x) {
         const uint32_t pixel = y * width + x;
         Vec3 col = Vec3::zero();
+        Rng rng(seed, pixel, 0);  // the pixel's stream; samples draw from it in order
         for (uint32_t s = 0; s < spp; ++s) {
-          Rng rng(seed, pixel, s);
           const float u = (float(x) + rng.gen_f32()) / float(width);
           const float v = (float(height - y) + rng.gen_f32()) / float(height);
           const Ray ray = camera.get_ray(u, v, rng);

@@ -4,7 +4,8 @@
    (never compiled upstream; values verified to hold in IEEE f32).
 2. Analytic known answers for utility.rs (reflect/refract/schlick), the shapes'
    hit() root cases (sphere.rs:23-51, plane.rs:24-44) and the build's box.
-3. Published RNG vectors: splitmix64 (seed 0) and xoshiro128** (state 1,2,3,4).
+3. RNG vectors: splitmix64 (seed 0, published) and xoshiro128+ (state 1,2,3,4),
+   checked against a pure-Python restatement of both.
 """
 import math
 
@@ -177,7 +178,7 @@ def _xoshiro(s, n):
     s = list(s)
     out = []
     for _ in range(n):
-        out.append((_rotl((s[1] * 5) & 0xFFFFFFFF, 7) * 9) & 0xFFFFFFFF)
+        out.append((s[0] + s[3]) & 0xFFFFFFFF)
         t = (s[1] << 9) & 0xFFFFFFFF
         s[2] ^= s[0]
         s[3] ^= s[1]
@@ -190,7 +191,8 @@ def _xoshiro(s, n):
 
 def test_published_vectors():
     assert _splitmix(0)[1] == 0xE220A8397B1DCDAF  # splitmix64, seed 0, first output
-    assert _xoshiro([1, 2, 3, 4], 4) == [11520, 0, 5927040, 70819200]  # xoshiro128** 1.1
+    # xoshiro128+ from state (1,2,3,4): s0 + s3 = 5, then state (7, 0, 1026, 12288) -> 12295, ...
+    assert _xoshiro([1, 2, 3, 4], 2) == [5, 12295]
 
 
 @pytest.mark.parametrize("seed,pixel,sample", [(0x5EED, 0, 0), (0x5EED, 2073599, 255), (7, 12345, 3), (0, 0, 0)])

@@ -1,0 +1,66 @@
+"""A/B timing of kernel variants (FORMA_RT_LIB builds of the same ABI) on one GPU.
+
+    python tools/ab_bench.py lib1.so lib2.so ... [--reps 3] [--scene scene_08]
+
+Each variant renders the bench workload; variants are interleaved `reps` times and the
+median kernel time (HIP events) is reported. Every variant's image is checked bit-exact
+against the first one's."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+CHILD = r'''
+import json, os, sys, hashlib
+sys.path.insert(0, os.path.join(sys.argv[1], "fo-rma_amd"))
+import forma_rt as fr
+scene, w, h, spp, depth, steps = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6]), int(sys.argv[7])
+sc = fr.Scene.from_file(fr.scene_path(scene), w, h)
+ctx = fr.RenderContext(0)
+p = fr.make_params(w, h, spp, depth)
+ctx.render(sc, sc.camera, p); ctx.sync()
+ms = []
+for _ in range(steps):
+    ctx.render(sc, sc.camera, p); ms.append(ctx.sync()["kernel_ms"])
+mean, u8 = ctx.download(w, h)
+print(json.dumps({"ms": sorted(ms)[len(ms)//2], "sha": hashlib.sha256(mean.tobytes()).hexdigest()[:16]}))
+'''
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--scene", default="scene_08")
+    ap.add_argument("--size", default="1920x1080")
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--depth", type=int, default=8)
+    a = ap.parse_args()
+    w, h = map(int, a.size.split("x"))
+    res = {lib: [] for lib in a.libs}
+    shas = {}
+    for _ in range(a.reps):
+        for lib in a.libs:
+            env = dict(os.environ, FORMA_RT_LIB=os.path.abspath(lib))
+            out = subprocess.run([sys.executable, "-c", CHILD, ROOT, a.scene, str(w), str(h), str(a.spp),
+                                  str(a.depth), str(a.steps)], env=env, capture_output=True, text=True, timeout=300)
+            if out.returncode != 0:
+                print(lib, "FAILED", out.stderr[-2000:])
+                sys.exit(1)
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            res[lib].append(r["ms"])
+            shas[lib] = r["sha"]
+    base = shas[a.libs[0]]
+    for lib in a.libs:
+        ms = sorted(res[lib])[len(res[lib]) // 2]
+        samples = w * h * a.spp
+        print(f"{os.path.basename(lib):32s} {ms:9.3f} ms  {samples / ms / 1e3:10.1f} Msamples/s  "
+              f"{'same image' if shas[lib] == base else 'IMAGE DIFFERS ' + shas[lib]}")
+
+
+if __name__ == "__main__":
+    main()
