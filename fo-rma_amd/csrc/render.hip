@@ -52,7 +52,7 @@ constexpr uint32_t kMaxDepth = 64;    // LDS stack bound (64 KB per workgroup)
 #ifndef FR_KREJ
 #define FR_KREJ 4  // rejection loop: lanes left to the next iteration (tuning only, results unchanged)
 #endif
-constexpr uint32_t kSmallDepth = 8;  // max_depth <= 8: attenuation-colour stack, unrolled unwind
+constexpr uint32_t kSmallDepth = 8;  // max_depth <= 8: u16 index stack, unrolled unwind
 
 // ABI layout, mirrored by ctypes (forma_rt.py) and the Rust binding
 static_assert(sizeof(fr_prim) == 88, "fr_prim layout");
@@ -66,10 +66,15 @@ struct DeviceCopy {
   void* blob = nullptr;
   uint32_t n = 0;
   bool has_plane = false;
+  uint32_t kinds = 0;  // bit k set if a primitive of kind k is present
   size_t off_kind = 0, off_g0 = 0, off_g1 = 0, off_g2 = 0, off_g3 = 0, off_mat = 0, off_cls = 0, off_att = 0;
+  size_t off_rec = 0;
 };
 
 struct KScene {
+  // one 64-B record per primitive (g0..g3; kind in the bits of g3.w): one scalar
+  // load brings a primitive into SGPRs in the closest-hit loop
+  const float4* __restrict__ rec;
   const uint32_t* __restrict__ kind;
   const float4* __restrict__ g0;
   const float4* __restrict__ g1;
@@ -146,21 +151,24 @@ __device__ __forceinline__ uint32_t lanes_set(bool b) { return static_cast<uint3
 //      (their draws stay in stream order, so results do not depend on KREJ);
 //   2. closest hit + shading for lanes holding a ray;
 //   3. path end: unwind the attenuations, accumulate, seed the next sample.
-// MAXD > 0: max_depth <= MAXD is known at compile time and the stack holds the
-// attenuation colours themselves (12 B per level), unwound by an unrolled,
-// predicated sequence; MAXD == 0: any max_depth, the stack holds primitive indices.
-template <bool HAS_PLANE, int KREJ, int MAXD>
+// MAXD > 0: max_depth <= MAXD is known at compile time; the stack holds u16 primitive
+// indices (n < 65536) and is unwound by an unrolled, predicated sequence.
+// MAXD == 0: any max_depth, u32 indices, a loop.
+// KS: KS_AABB / KS_SPHERE when every primitive has that kind (no per-primitive kind
+// switch), else KS_ANY.
+enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
+
+template <int KS, bool HAS_PLANE, int KREJ, int MAXD>
 __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KParams kp,
                                                         float* __restrict__ out_mean,
                                                         uint8_t* __restrict__ out_u8,
                                                         unsigned long long* __restrict__ counters) {
-  // LDS: [attenuation rgb, n_att entries][stack: MAXD ? MAXD x 3 x kBlock f32 attenuations
-  //                                              : max_depth x kBlock primitive indices]
+  // LDS: [attenuation rgb, n_att entries][stack: MAXD ? MAXD x kBlock u16 : max_depth x kBlock u32]
   extern __shared__ uint32_t lds[];
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
   float* att_lds = reinterpret_cast<float*>(lds);
   uint32_t* stack = lds + n_att * 3u;
-  float* astack = reinterpret_cast<float*>(stack);
+  uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < n_att; i += kBlock) {
     const float4 a = sc.att[i];
@@ -199,14 +207,10 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
   };
   // stack push at level `depth` of the scatter winner
   auto push = [&](uint32_t pi) {
-    if (MAXD > 0) {
-      const V3 a = att_of(pi);
-      astack[(depth * 3 + 0) * kBlock + tid] = a.x;
-      astack[(depth * 3 + 1) * kBlock + tid] = a.y;
-      astack[(depth * 3 + 2) * kBlock + tid] = a.z;
-    } else {
+    if (MAXD > 0)
+      hstack[depth * kBlock + tid] = static_cast<uint16_t>(pi);
+    else
       stack[depth * kBlock + tid] = pi;
-    }
   };
   V3 sum{0.0f, 0.0f, 0.0f};
   // the ray; while a lens sample is pending d.xy = (u, v); while a scatter sample is
@@ -290,20 +294,23 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
       float closest = FLT_MAX, t_last = 0.0f;
       int best = -1;
       for (uint32_t i = 0; i < sc.n; ++i) {
-        const uint32_t k = sc.kind[i];  // wave-uniform: scalar branch
+        const float4* r4 = sc.rec + 4 * i;  // wave-uniform address: scalar loads
+        const uint32_t k = KS == KS_AABB ? FR_AABB
+                           : KS == KS_SPHERE ? FR_SPHERE
+                                             : __float_as_uint(r4[3].w);  // scalar branch
         float t = 0.0f;
         bool h = false;
         if (k == FR_AABB) {
-          h = slab_root(slab3(xyz(sc.g0[i]), xyz(sc.g1[i]), o, inv), 0.001f, closest, t);
+          h = slab_root(slab3(xyz(r4[0]), xyz(r4[1]), o, inv), 0.001f, closest, t);
         } else if (k == FR_SPHERE) {
-          const float4 g = sc.g0[i];
+          const float4 g = r4[0];
           h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, closest, t);
         } else if (k == FR_PLANE) {
-          const int r = plane_test(xyz(sc.g0[i]), xyz(sc.g1[i]), xyz(sc.g2[i]), o, d, 0.001f, closest, t);
+          const int r = plane_test(xyz(r4[0]), xyz(r4[1]), xyz(r4[2]), o, d, 0.001f, closest, t);
           if (r) t_last = t;
           h = r == 2;
         } else if (k == FR_OBB) {
-          const float4 a = sc.g0[i], b = sc.g1[i], c = sc.g2[i], e = sc.g3[i];
+          const float4 a = r4[0], b = r4[1], c = r4[2], e = r4[3];
           const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
           h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, closest, t);
         }
@@ -325,8 +332,9 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
         if (depth < kp.max_depth) {
           // the shared HitRecord: normal of the winner at its own t; p = point_at(last t written)
           const V3 pw = add(o, scl(closest, d));
-          const uint32_t kb = sc.kind[best];
-          const float4 b0 = sc.g0[best], b1 = sc.g1[best];
+          const float4* rb = sc.rec + 4 * best;
+          const uint32_t kb = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(rb[3].w);
+          const float4 b0 = rb[0], b1 = rb[1];
           V3 n;
           if (kb == FR_AABB) {
             n = slab_normal(slab3(xyz(b0), xyz(b1), o, inv), closest, d);
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
           } else if (kb == FR_PLANE) {
             n = scl(-1.0f, xyz(b1));
           } else {
-            const float4 b2 = sc.g2[best], b3 = sc.g3[best];
+            const float4 b2 = rb[2], b3 = rb[3];
             const ObbFrame f = obb_frame(xyz(b0), xyz(b1), xyz(b2), xyz(b3), o, d);
             const Slab sl = slab3(V3{-b0.w, -b1.w, -b2.w}, V3{b0.w, b1.w, b2.w}, f.ol, f.inv);
             n = obb_normal(xyz(b1), xyz(b2), xyz(b3), sl, closest, f.dl);
@@ -380,9 +388,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
           if (j < static_cast<int>(depth)) {
             DIAG_WAVE(DG_UNW_W);
             DIAG_LANE(DG_UNW_L);
-            const V3 a{astack[(j * 3 + 0) * kBlock + tid], astack[(j * 3 + 1) * kBlock + tid],
-                       astack[(j * 3 + 2) * kBlock + tid]};
-            col = mul(a, col);
+            col = mul(att_of(hstack[j * kBlock + tid]), col);
           }
         }
       } else {
@@ -504,6 +510,8 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   off = align_up(off + m * 4, 256);
   c->off_att = off;
   off = align_up(off + m * 16, 256);
+  c->off_rec = off;
+  off = align_up(off + m * 64, 256);
   std::vector<unsigned char> host(off, 0);
   for (uint32_t i = 0; i < n; ++i) {
     const fr_prim& p = s->prims[i];
@@ -540,16 +548,23 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
     memcpy(&host[c->off_mat + 16 * i], &mat, 16);
     memcpy(&host[c->off_cls + 4 * i], &cls, 4);
     memcpy(&host[c->off_att + 16 * i], &att, 16);
+    memcpy(&g[3].w, &kind, 4);  // kind bits in g3.w
+    memcpy(&host[c->off_rec + 64 * i], g, 64);
   }
   if (n == 0) {
     const uint32_t stub = FR_STUB;
     memcpy(&host[c->off_kind], &stub, 4);
+    memcpy(&host[c->off_rec + 60], &stub, 4);
   }
   HIPCHK(hipMalloc(&c->blob, off));
   HIPCHK(hipMemcpy(c->blob, host.data(), off, hipMemcpyHostToDevice));
   c->n = n;
   c->has_plane = false;
-  for (const fr_prim& p : s->prims) c->has_plane |= p.kind == FR_PLANE;
+  c->kinds = 0;
+  for (const fr_prim& p : s->prims) {
+    c->has_plane |= p.kind == FR_PLANE;
+    c->kinds |= 1u << (p.kind <= FR_STUB ? p.kind : FR_STUB);
+  }
   c->version = s->version;
   *out = c;
   return FR_OK;
@@ -589,6 +604,31 @@ struct fr_ctx {
   bool pending = false;
   std::chrono::steady_clock::time_point t0;
 };
+
+// Picks the specialisation: single-kind scenes (all boxes, all spheres) drop the
+// per-primitive kind switch; HAS_PLANE adds the stale-record bookkeeping; small depth
+// uses the colour stack.
+template <int KS, bool HP>
+static void launch_depth(bool small_depth, dim3 g, size_t lds, hipStream_t st, const KScene& ks, const KCam& kc,
+                         const KParams& kp, float* m, uint8_t* u, unsigned long long* cnt) {
+  if (small_depth)
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth>), g, dim3(kBlock), lds, st, ks, kc, kp, m, u, cnt);
+  else
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0>), g, dim3(kBlock), lds, st, ks, kc, kp, m, u, cnt);
+}
+
+static void launch_trace(uint32_t kinds, bool has_plane, bool small_depth, dim3 g, size_t lds, hipStream_t st,
+                         const KScene& ks, const KCam& kc, const KParams& kp, float* m, uint8_t* u,
+                         unsigned long long* cnt) {
+  if (kinds == (1u << FR_AABB))
+    launch_depth<KS_AABB, false>(small_depth, g, lds, st, ks, kc, kp, m, u, cnt);
+  else if (kinds == (1u << FR_SPHERE))
+    launch_depth<KS_SPHERE, false>(small_depth, g, lds, st, ks, kc, kp, m, u, cnt);
+  else if (has_plane)
+    launch_depth<KS_ANY, true>(small_depth, g, lds, st, ks, kc, kp, m, u, cnt);
+  else
+    launch_depth<KS_ANY, false>(small_depth, g, lds, st, ks, kc, kp, m, u, cnt);
+}
 
 static int check_params(const fr_params* p) {
   if (!p) return set_error(FR_EARG, "null params");
@@ -676,6 +716,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   }
   KScene ks;
   const char* b = static_cast<const char*>(dc->blob);
+  ks.rec = reinterpret_cast<const float4*>(b + dc->off_rec);
   ks.kind = reinterpret_cast<const uint32_t*>(b + dc->off_kind);
   ks.g0 = reinterpret_cast<const float4*>(b + dc->off_g0);
   ks.g1 = reinterpret_cast<const float4*>(b + dc->off_g1);
@@ -716,23 +757,13 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   if (kp.n_tiles) {
     const uint32_t blocks = (kp.n_tiles + 3u) / 4u;
     const size_t n_att = dc->n <= kAttLds ? dc->n : 0u;
-    const bool small_depth = p->max_depth <= kSmallDepth;
-    const size_t stack_bytes = small_depth ? kSmallDepth * 3 * kBlock * sizeof(float)
-                                           : static_cast<size_t>(p->max_depth) * kBlock * sizeof(uint32_t);
+    const bool small_depth = p->max_depth <= kSmallDepth && dc->n < 65536u;
+    const size_t stack_bytes = small_depth ? kSmallDepth * kBlock * sizeof(uint16_t)
+                                           : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
+                                                 sizeof(uint32_t);
     const size_t lds = n_att * 3 * sizeof(float) + stack_bytes;
-    const dim3 g(blocks), b(kBlock);
-    if (dc->has_plane && small_depth)
-      hipLaunchKernelGGL((trace_kernel<true, FR_KREJ, kSmallDepth>), g, b, lds, c->stream, ks, kc, kp, c->d_mean,
-                         c->d_u8, c->d_cnt);
-    else if (dc->has_plane)
-      hipLaunchKernelGGL((trace_kernel<true, FR_KREJ, 0>), g, b, lds, c->stream, ks, kc, kp, c->d_mean, c->d_u8,
-                         c->d_cnt);
-    else if (small_depth)
-      hipLaunchKernelGGL((trace_kernel<false, FR_KREJ, kSmallDepth>), g, b, lds, c->stream, ks, kc, kp, c->d_mean,
-                         c->d_u8, c->d_cnt);
-    else
-      hipLaunchKernelGGL((trace_kernel<false, FR_KREJ, 0>), g, b, lds, c->stream, ks, kc, kp, c->d_mean, c->d_u8,
-                         c->d_cnt);
+    launch_trace(dc->kinds, dc->has_plane, small_depth, dim3(blocks), lds, c->stream, ks, kc, kp, c->d_mean,
+                 c->d_u8, c->d_cnt);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(c->ev1, c->stream));

@@ -232,11 +232,12 @@ FR_HD Slab slab3(V3 lo, V3 hi, V3 o, V3 inv) {
 }
 
 // Root selection: returns true and the accepted t if the box is hit in (t_min, t_max).
+// Equivalent branch-free form of "near root if tn in (t_min, t_max), else far root if
+// tf in (t_min, t_max), and tn < tf": when tn > t_min the far root can only be taken
+// if tn >= t_max, and then tf > tn >= t_max fails too.
 FR_HD bool slab_root(const Slab& s, float t_min, float t_max, float& t) {
-  const bool c1 = s.tn > t_min && s.tn < t_max;
-  const bool c2 = s.tf > t_min && s.tf < t_max;
-  t = c1 ? s.tn : s.tf;
-  return s.tn < s.tf && (c1 || c2);
+  t = s.tn > t_min ? s.tn : s.tf;
+  return (t > t_min) & (t < t_max) & (s.tn < s.tf);
 }
 
 FR_HD float comp(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
