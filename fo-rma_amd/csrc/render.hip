@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <chrono>
 #include <thread>
@@ -32,6 +33,8 @@ __device__ unsigned long long g_fr_diag_rus[2];
       atomicAdd(&arr[1], static_cast<unsigned long long>(__popcll(m_)));           \
     }                                                                              \
   } while (0)
+// per-wave start/end (s_memrealtime, 100 MHz) for the residency-over-time profile
+__device__ unsigned long long g_fr_wave_times[2 * 65536];
 #define FR_LENS_TRY() FR_DIAG_TRY(g_fr_diag_lens)
 #define FR_RUS_TRY() FR_DIAG_TRY(g_fr_diag_rus)
 #endif
@@ -52,13 +55,18 @@ constexpr uint32_t kMaxDepth = 64;    // LDS stack bound (64 KB per workgroup)
 #ifndef FR_KREJ
 #define FR_KREJ 4  // rejection loop: lanes left to the next iteration (tuning only, results unchanged)
 #endif
-constexpr uint32_t kSmallDepth = 8;  // max_depth <= 8: u16 index stack, unrolled unwind
+#ifndef FR_NUM_SGPR
+#define FR_NUM_SGPR 96
+#endif
+constexpr uint32_t kSmallDepth = 8;
+constexpr uint32_t kBlockSamples = 16;  // samples per RNG stream (numerics contract)
+constexpr uint64_t kBatch = 64;         // work items claimed per global atomic (one tile, one block)  // max_depth <= 8: u16 index stack, unrolled unwind
 
 // ABI layout, mirrored by ctypes (forma_rt.py) and the Rust binding
 static_assert(sizeof(fr_prim) == 88, "fr_prim layout");
 static_assert(sizeof(fr_camera) == 104, "fr_camera layout");
 static_assert(sizeof(fr_params) == 40, "fr_params layout");
-static_assert(sizeof(fr_stats) == 48, "fr_stats layout");
+static_assert(sizeof(fr_stats) == 56, "fr_stats layout");
 
 struct DeviceCopy {
   int device = -1;
@@ -90,6 +98,16 @@ struct KParams {
   uint32_t W, H, spp, max_depth;
   uint64_t seed;
   uint32_t shard_index, shard_count, tiles_per_row, n_tiles, flags;
+  uint32_t P;         // pixel slots of the shard: n_tiles x 64, tile order
+  uint32_t b0, nb;    // this pass renders sample blocks [b0, b0 + nb)
+  uint64_t n_items;   // nb x P work items (pixel slot, block)
+};
+
+// Work buffers of one render pass.
+struct KWork {
+  unsigned long long* queue;  // next unclaimed item (zeroed before the pass)
+  float* samples;             // per-sample colours, [(s - 16*b0) * P + q] x 3 f32
+  unsigned long long* counters;
 };
 
 // camera.rs fields the ray generator reads: position, lower_left_corner,
@@ -112,6 +130,20 @@ static uint32_t scatter_class(const fr_prim& p) {
 }
 
 __device__ __forceinline__ V3 xyz(float4 a) { return V3{a.x, a.y, a.z}; }
+
+// The scene is read-only for the kernel's lifetime: reading it through the constant
+// address space lets the compiler use scalar loads even though the kernel stores to
+// global memory inside the same loop.
+typedef __attribute__((address_space(4))) const float cfloat;
+struct RecRef {  // the 4 float4 of one primitive record, read through addrspace(4)
+  cfloat* p;
+  __device__ __forceinline__ float4 operator[](int k) const {
+    return make_float4(p[4 * k], p[4 * k + 1], p[4 * k + 2], p[4 * k + 3]);
+  }
+};
+__device__ __forceinline__ RecRef rec_at(const float4* base, uint32_t i) {
+  return RecRef{(cfloat*)(reinterpret_cast<uintptr_t>(base)) + 16u * i};
+}
 
 constexpr uint32_t kAttLds = 1024;  // attenuation table entries staged in LDS
 
@@ -140,17 +172,37 @@ enum { DG_ITER, DG_REGEN_W, DG_REGEN_L, DG_LENS_W, DG_LENS_L, DG_RUS_W, DG_RUS_L
 // the last written t is tracked separately from the winner's.
 __device__ __forceinline__ uint32_t lanes_set(bool b) { return static_cast<uint32_t>(__popcll(__ballot(b))); }
 
-// Per iteration of the lane loop (each lane owns one pixel and walks its samples in
-// order, so its f32 sum keeps the reference's sample order):
+// Pixel slot q of a shard -> image coordinates. Slots run tile by tile (8x8 pixels,
+// tiles left to right within an 8-row strip, the shard's strips top to bottom); slots
+// past the image edge are invalid.
+__device__ __forceinline__ bool slot_xy(const KParams& kp, uint32_t q, uint32_t& x, uint32_t& y) {
+  const uint32_t tile = q >> 6, l = q & 63u;
+  const uint32_t ls = tile / kp.tiles_per_row;
+  const uint32_t tc = tile - ls * kp.tiles_per_row;
+  const uint32_t strip = kp.shard_index + ls * kp.shard_count;
+  x = tc * 8u + (l & 7u);
+  y = strip * kStripRows + (l >> 3);
+  return x < kp.W && y < kp.H;
+}
+
+// Persistent path-tracing kernel. Work item = (pixel slot q, sample block b): the
+// kBlockSamples samples [16b, 16b + 16) of one pixel, drawn in order from the RNG
+// stream (seed, pixel, b). Each sample's colour goes to kw.samples; sum_kernel then
+// adds every pixel's samples in sample order, exactly as save_image's
+// `col = col + get_color(...)` (tracer.rs:170-175). Items are independent, so lanes
+// never wait for one another's pixels: a wave claims 64 items (one tile, one block)
+// per global atomic and hands them to its free lanes (ballot + mbcnt).
+//
+// Per iteration of the lane loop:
+//   0. lanes without an item claim one;
 //   1. one merged rejection loop serves both random_in_unit_circle (lens sample of a
 //      new camera ray, utility.rs:4-13) and random_in_unit_sphere (scatter,
 //      utility.rs:15-25): a circle try is a sphere try without the third draw, and
-//      dot(p,p) = (px*px + py*py) + 0 is the same value. Lanes of both kinds share the
-//      SIMT trips instead of running two loops. The loop stops once at most KREJ lanes
-//      of the wave still reject; those keep their RNG state and go on next iteration
-//      (their draws stay in stream order, so results do not depend on KREJ);
+//      dot(p,p) = (px*px + py*py) + 0 is the same value. It stops once at most KREJ
+//      lanes still reject; those keep their RNG state and go on next iteration (their
+//      draws stay in stream order, so results do not depend on KREJ);
 //   2. closest hit + shading for lanes holding a ray;
-//   3. path end: unwind the attenuations, accumulate, seed the next sample.
+//   3. path end: unwind the attenuations, store the sample colour, next sample.
 // MAXD > 0: max_depth <= MAXD is known at compile time; the stack holds u16 primitive
 // indices (n < 65536) and is unwound by an unrolled, predicated sequence.
 // MAXD == 0: any max_depth, u32 indices, a loop.
@@ -158,47 +210,43 @@ __device__ __forceinline__ uint32_t lanes_set(bool b) { return static_cast<uint3
 // switch), else KS_ANY.
 enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 
+// amdgpu_num_sgpr caps the scalar registers (MI355X_MICROARCH.md "Residency and
+// cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
+// admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
 template <int KS, bool HAS_PLANE, int KREJ, int MAXD>
-__global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KParams kp,
-                                                        float* __restrict__ out_mean,
-                                                        uint8_t* __restrict__ out_u8,
-                                                        unsigned long long* __restrict__ counters) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) void trace_kernel(
+    KScene sc, KCam cam, KParams kp, KWork kw) {
   // LDS: [attenuation rgb, n_att entries][stack: MAXD ? MAXD x kBlock u16 : max_depth x kBlock u32]
   extern __shared__ uint32_t lds[];
+  __shared__ unsigned long long wq_next[kBlock / 64], wq_end[kBlock / 64];  // per-wave item batch
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
   float* att_lds = reinterpret_cast<float*>(lds);
   uint32_t* stack = lds + n_att * 3u;
   uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
   const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u, wave = tid >> 6;
   for (uint32_t i = tid; i < n_att; i += kBlock) {
     const float4 a = sc.att[i];
     att_lds[3 * i + 0] = a.x;
     att_lds[3 * i + 1] = a.y;
     att_lds[3 * i + 2] = a.z;
   }
+  if (lane == 0) {
+    wq_next[wave] = 0;
+    wq_end[wave] = 0;
+  }
 #ifdef FR_DIAG
   __shared__ uint32_t dg[DG_N];
   if (tid < DG_N) dg[tid] = 0;
+  const uint32_t gw = blockIdx.x * (kBlock / 64u) + wave;
+  if (lane == 0 && gw < 65536) g_fr_wave_times[2 * gw] = __builtin_amdgcn_s_memrealtime();
 #endif
   __syncthreads();
 
-  const uint32_t lane = tid & 63u;
-  const uint32_t tile = blockIdx.x * (kBlock / 64u) + (tid >> 6);
-  uint32_t x = 0, y = 0;
-  bool valid = false;
-  if (tile < kp.n_tiles) {
-    const uint32_t ls = tile / kp.tiles_per_row;
-    const uint32_t tc = tile - ls * kp.tiles_per_row;
-    const uint32_t strip = kp.shard_index + ls * kp.shard_count;
-    x = tc * 8u + (lane & 7u);
-    y = strip * kStripRows + (lane >> 3);
-    valid = x < kp.W && y < kp.H;
-  }
-  const uint32_t pixel = y * kp.W + x;
   const V3 cpos{cam.px, cam.py, cam.pz}, cllc{cam.lx, cam.ly, cam.lz}, chor{cam.hx, cam.hy, cam.hz};
   const V3 cver{cam.vx, cam.vy, cam.vz}, cu{cam.ux, cam.uy, cam.uz}, cv{cam.bx, cam.by, cam.bz};
   const float fW = static_cast<float>(kp.W), fH = static_cast<float>(kp.H);
-  const float fx = static_cast<float>(x), fy = static_cast<float>(kp.H - y);  // tracer.rs:171-172
+  const uint32_t s_pass = kp.b0 * kBlockSamples;
 
   enum : uint32_t { NEED_NONE = 0, NEED_LENS = 1, NEED_SPHERE = 2 };
   uint32_t depth = 0;
@@ -212,30 +260,62 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
     else
       stack[depth * kBlock + tid] = pi;
   };
-  V3 sum{0.0f, 0.0f, 0.0f};
+
   // the ray; while a lens sample is pending d.xy = (u, v); while a scatter sample is
   // pending o = hit point and d = scatter base ((p + n), or reflect(unit(d), n) for metal)
   V3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
   V3 sn{0.0f, 0.0f, 0.0f};  // metal: normal
-  float sfuzz = 0.0f;
+  float sfuzz = 0.0f, fx = 0.0f, fy = 0.0f;
   bool smetal = false;
-  uint32_t sbest = 0;
+  uint32_t sbest = 0, q = 0, s = 0, s_end = 0, nseg = 0, nhit = 0;
   Rng rng{0u, 0u, 0u, 0u};
-  uint32_t s = 0, nseg = 0, nhit = 0;
-  bool active = valid && kp.spp > 0;
-  bool have_ray = false;
+  bool active = true, need_item = true, have_ray = false;
   uint32_t need = NEED_NONE;
-  if (active) {
-    rng = rng_seed(kp.seed, pixel, 0u);  // the pixel's stream, drawn in sample order
-    const float r0 = rng_f32(rng);
-    const float r1 = rng_f32(rng);
-    d.x = (fx + r0) / fW;
-    d.y = (fy + r1) / fH;
-    need = NEED_LENS;
-  }
 
   while (active) {
     DIAG_WAVE(DG_ITER);
+    if (need_item) {
+      // 0. claim a work item: the free lanes take consecutive items of the wave's
+      // batch; when it runs out, the first free lane claims the next 64 globally
+      const unsigned long long m = __ballot(1);
+      const uint32_t n = static_cast<uint32_t>(__popcll(m));
+      const uint32_t r = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+      const unsigned long long next = wq_next[wave], end = wq_end[wave];
+      const unsigned long long avail = end - next;
+      unsigned long long base = 0;
+      if (n > avail) {
+        if (r == 0) base = atomicAdd(kw.queue, static_cast<unsigned long long>(kBatch));
+        base = __builtin_amdgcn_readfirstlane(base);
+      }
+      const unsigned long long item = r < avail ? next + r : base + (r - avail);
+      if (r == 0) {
+        wq_next[wave] = n > avail ? base + (n - avail) : next + n;
+        if (n > avail) wq_end[wave] = base + kBatch;
+      }
+      if (item >= kp.n_items) {
+        active = false;  // queue drained
+        continue;
+      }
+      const uint32_t b = kp.b0 + static_cast<uint32_t>(item / kp.P);
+      q = static_cast<uint32_t>(item % kp.P);
+      uint32_t x, y;
+      if (slot_xy(kp, q, x, y)) {
+        const uint32_t pixel = y * kp.W + x;
+        rng = rng_seed(kp.seed, pixel, b);  // this block's stream
+        s = b * kBlockSamples;
+        s_end = min(s + kBlockSamples, kp.spp);
+        fx = static_cast<float>(x);
+        fy = static_cast<float>(kp.H - y);  // tracer.rs:171-172
+        // first sample of the block: jitter; the lens sample follows in step 1
+        const float r0 = rng_f32(rng);
+        const float r1 = rng_f32(rng);
+        d.x = (fx + r0) / fW;
+        d.y = (fy + r1) / fH;
+        need = NEED_LENS;
+        need_item = false;
+      }
+    }
     bool ended = false;
     V3 term{0.0f, 0.0f, 0.0f};
     if (need != NEED_NONE) {
@@ -293,8 +373,10 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
       const float a_dd = dot(d, d);
       float closest = FLT_MAX, t_last = 0.0f;
       int best = -1;
-      for (uint32_t i = 0; i < sc.n; ++i) {
-        const float4* r4 = sc.rec + 4 * i;  // wave-uniform address: scalar loads
+      for (uint32_t ii = 0; ii < sc.n; ++ii) {
+        // the index is wave-uniform; say so, or the compiler may fall back to vector loads
+        const uint32_t i = __builtin_amdgcn_readfirstlane(ii);
+        const RecRef r4 = rec_at(sc.rec, i);  // scalar loads
         const uint32_t k = KS == KS_AABB ? FR_AABB
                            : KS == KS_SPHERE ? FR_SPHERE
                                              : __float_as_uint(r4[3].w);  // scalar branch
@@ -398,11 +480,14 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
           col = mul(att_of(stack[j * kBlock + tid]), col);
         }
       }
-      sum = add(sum, col);
-      if (++s == kp.spp) {
-        active = false;
+      float* out = kw.samples + 3 * (static_cast<size_t>(s - s_pass) * kp.P + q);
+      out[0] = col.x;
+      out[1] = col.y;
+      out[2] = col.z;
+      if (++s == s_end) {
+        need_item = true;
       } else {
-        // next sample: jitter (tracer.rs:171-172); the lens sample follows in step 1
+        // next sample of the block: jitter (tracer.rs:171-172), same stream
         const float r0 = rng_f32(rng);
         const float r1 = rng_f32(rng);
         d.x = (fx + r0) / fW;
@@ -412,18 +497,6 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
     }
   }
 
-  if (valid) {
-    const V3 mean = divs(sum, static_cast<float>(kp.spp));  // tracer.rs:177
-    const size_t idx = static_cast<size_t>(pixel) * 3u;
-    out_mean[idx + 0] = mean.x;
-    out_mean[idx + 1] = mean.y;
-    out_mean[idx + 2] = mean.z;
-    if (kp.flags & FR_FLAG_WRITE_U8) {
-      out_u8[idx + 0] = to_u8(mean.x);
-      out_u8[idx + 1] = to_u8(mean.y);
-      out_u8[idx + 2] = to_u8(mean.z);
-    }
-  }
   // per-wave counter reduction, one 64-bit atomic per wave per counter
   unsigned long long a = nseg, b = nhit;
   for (int m = 32; m > 0; m >>= 1) {
@@ -431,13 +504,49 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(KScene sc, KCam cam, KPar
     b += __shfl_xor(b, m);
   }
   if (lane == 0 && (a | b)) {
-    atomicAdd(&counters[0], a);
-    atomicAdd(&counters[1], b);
+    atomicAdd(&kw.counters[0], a);
+    atomicAdd(&kw.counters[1], b);
   }
 #ifdef FR_DIAG
+  if (lane == 0 && gw < 65536) g_fr_wave_times[2 * gw + 1] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
-  if (tid < DG_N) atomicAdd(&counters[4 + tid], static_cast<unsigned long long>(dg[tid]));
+  if (tid < DG_N) atomicAdd(&kw.counters[4 + tid], static_cast<unsigned long long>(dg[tid]));
 #endif
+}
+
+// Adds each pixel's sample colours of this pass, in sample order, onto its running
+// sum (tracer.rs:174); the last pass divides by spp, gamma-corrects and quantises
+// (tracer.rs:177-184). One thread per pixel slot; reads are coalesced across slots.
+__global__ __launch_bounds__(256) void sum_kernel(KParams kp, const float* __restrict__ samples,
+                                                  float* __restrict__ running, float* __restrict__ out_mean,
+                                                  uint8_t* __restrict__ out_u8, int first, int last) {
+  const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+  if (q >= kp.P) return;
+  uint32_t x, y;
+  if (!slot_xy(kp, q, x, y)) return;
+  V3 sum = first ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
+  const uint32_t s0 = kp.b0 * kBlockSamples;
+  const uint32_t s1 = min((kp.b0 + kp.nb) * kBlockSamples, kp.spp);
+  for (uint32_t s = s0; s < s1; ++s) {
+    const float* c = samples + 3 * (static_cast<size_t>(s - s0) * kp.P + q);
+    sum = add(sum, V3{c[0], c[1], c[2]});
+  }
+  if (!last) {
+    running[3 * q] = sum.x;
+    running[3 * q + 1] = sum.y;
+    running[3 * q + 2] = sum.z;
+    return;
+  }
+  const V3 mean = divs(sum, static_cast<float>(kp.spp));  // tracer.rs:177
+  const size_t idx = (static_cast<size_t>(y) * kp.W + x) * 3u;
+  out_mean[idx + 0] = mean.x;
+  out_mean[idx + 1] = mean.y;
+  out_mean[idx + 2] = mean.z;
+  if (kp.flags & FR_FLAG_WRITE_U8) {
+    out_u8[idx + 0] = to_u8(mean.x);
+    out_u8[idx + 1] = to_u8(mean.y);
+    out_u8[idx + 2] = to_u8(mean.z);
+  }
 }
 
 // ---- diagnostics kernels ---------------------------------------------------
@@ -595,10 +704,15 @@ struct fr_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> ev_trace;  // start/stop pairs around each pass's trace kernel
+  int passes = 0;
   float* d_mean = nullptr;
   uint8_t* d_u8 = nullptr;
-  unsigned long long* d_cnt = nullptr;
-  size_t cap_pixels = 0;
+  unsigned long long* d_cnt = nullptr;  // [0..3] counters, [4..] diagnostics; [31] queue head
+  float* d_samples = nullptr;
+  float* d_running = nullptr;
+  size_t cap_pixels = 0, cap_samples = 0, cap_running = 0;
+  int num_cus = 0;
   fr_params last{};
   uint32_t last_n = 0;
   bool pending = false;
@@ -607,27 +721,34 @@ struct fr_ctx {
 
 // Picks the specialisation: single-kind scenes (all boxes, all spheres) drop the
 // per-primitive kind switch; HAS_PLANE adds the stale-record bookkeeping; small depth
-// uses the colour stack.
+// uses the u16 stack with the unrolled unwind.
 template <int KS, bool HP>
 static void launch_depth(bool small_depth, dim3 g, size_t lds, hipStream_t st, const KScene& ks, const KCam& kc,
-                         const KParams& kp, float* m, uint8_t* u, unsigned long long* cnt) {
+                         const KParams& kp, const KWork& kw) {
   if (small_depth)
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth>), g, dim3(kBlock), lds, st, ks, kc, kp, m, u, cnt);
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
   else
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0>), g, dim3(kBlock), lds, st, ks, kc, kp, m, u, cnt);
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
 }
 
 static void launch_trace(uint32_t kinds, bool has_plane, bool small_depth, dim3 g, size_t lds, hipStream_t st,
-                         const KScene& ks, const KCam& kc, const KParams& kp, float* m, uint8_t* u,
-                         unsigned long long* cnt) {
+                         const KScene& ks, const KCam& kc, const KParams& kp, const KWork& kw) {
   if (kinds == (1u << FR_AABB))
-    launch_depth<KS_AABB, false>(small_depth, g, lds, st, ks, kc, kp, m, u, cnt);
+    launch_depth<KS_AABB, false>(small_depth, g, lds, st, ks, kc, kp, kw);
   else if (kinds == (1u << FR_SPHERE))
-    launch_depth<KS_SPHERE, false>(small_depth, g, lds, st, ks, kc, kp, m, u, cnt);
+    launch_depth<KS_SPHERE, false>(small_depth, g, lds, st, ks, kc, kp, kw);
   else if (has_plane)
-    launch_depth<KS_ANY, true>(small_depth, g, lds, st, ks, kc, kp, m, u, cnt);
+    launch_depth<KS_ANY, true>(small_depth, g, lds, st, ks, kc, kp, kw);
   else
-    launch_depth<KS_ANY, false>(small_depth, g, lds, st, ks, kc, kp, m, u, cnt);
+    launch_depth<KS_ANY, false>(small_depth, g, lds, st, ks, kc, kp, kw);
+}
+
+// Bytes of per-sample colours one pass may hold (FR_SAMPLE_BUFFER_GB, default 8).
+static size_t sample_buffer_cap() {
+  double gb = 8.0;
+  if (const char* e = getenv("FR_SAMPLE_BUFFER_GB")) gb = atof(e);
+  if (gb < 0.001) gb = 0.001;
+  return static_cast<size_t>(gb * (1ull << 30));
 }
 
 static int check_params(const fr_params* p) {
@@ -673,6 +794,9 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
     }
     c->own_stream = true;
   }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  if (c->num_cus <= 0) c->num_cus = 256;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipMalloc(&c->d_cnt, 32 * sizeof(unsigned long long)) != hipSuccess) {
     fr_ctx_free(c);
@@ -689,6 +813,9 @@ void fr_ctx_free(fr_ctx* c) {
   if (c->d_mean) (void)hipFree(c->d_mean);
   if (c->d_u8) (void)hipFree(c->d_u8);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
+  if (c->d_samples) (void)hipFree(c->d_samples);
+  if (c->d_running) (void)hipFree(c->d_running);
+  for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -744,6 +871,44 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   const uint32_t my_strips =
       strips > p->shard_index ? (strips - p->shard_index + p->shard_count - 1) / p->shard_count : 0u;
   kp.n_tiles = my_strips * kp.tiles_per_row;
+  kp.P = kp.n_tiles * 64u;
+  const uint32_t nblocks = (p->spp + kBlockSamples - 1) / kBlockSamples;
+  // passes: as many sample blocks per pass as the sample buffer holds
+  const size_t per_block = static_cast<size_t>(kp.P) * kBlockSamples * 3 * sizeof(float);
+  uint32_t nb_pass = per_block ? static_cast<uint32_t>(sample_buffer_cap() / per_block) : nblocks;
+  if (nb_pass < 1) nb_pass = 1;
+  if (nb_pass > nblocks) nb_pass = nblocks;
+  const int passes = nblocks ? static_cast<int>((nblocks + nb_pass - 1) / nb_pass) : 0;
+  if (kp.P && nb_pass && per_block * nb_pass > c->cap_samples) {
+    if (c->d_samples) HIPCHK(hipFree(c->d_samples));
+    c->d_samples = nullptr;
+    c->cap_samples = 0;
+    HIPCHK(hipMalloc(&c->d_samples, per_block * nb_pass));
+    c->cap_samples = per_block * nb_pass;
+  }
+  const size_t running_bytes = static_cast<size_t>(kp.P) * 3 * sizeof(float);
+  if (passes > 1 && running_bytes > c->cap_running) {
+    if (c->d_running) HIPCHK(hipFree(c->d_running));
+    c->d_running = nullptr;
+    c->cap_running = 0;
+    HIPCHK(hipMalloc(&c->d_running, running_bytes));
+    c->cap_running = running_bytes;
+  }
+  while (c->ev_trace.size() < 2u * static_cast<size_t>(passes)) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    c->ev_trace.push_back(e);
+  }
+  const size_t n_att = dc->n <= kAttLds ? dc->n : 0u;
+  const bool small_depth = p->max_depth <= kSmallDepth && dc->n < 65536u;
+  const size_t stack_bytes = small_depth ? kSmallDepth * kBlock * sizeof(uint16_t)
+                                         : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
+                                               sizeof(uint32_t);
+  const size_t lds = n_att * 3 * sizeof(float) + stack_bytes;
+  KWork kw;
+  kw.queue = c->d_cnt + 31;
+  kw.samples = c->d_samples;
+  kw.counters = c->d_cnt;
   c->t0 = std::chrono::steady_clock::now();
   HIPCHK(hipMemsetAsync(c->d_cnt, 0, 32 * sizeof(unsigned long long), c->stream));
 #ifdef FR_DIAG
@@ -754,18 +919,30 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   }
 #endif
   HIPCHK(hipEventRecord(c->ev0, c->stream));
-  if (kp.n_tiles) {
-    const uint32_t blocks = (kp.n_tiles + 3u) / 4u;
-    const size_t n_att = dc->n <= kAttLds ? dc->n : 0u;
-    const bool small_depth = p->max_depth <= kSmallDepth && dc->n < 65536u;
-    const size_t stack_bytes = small_depth ? kSmallDepth * kBlock * sizeof(uint16_t)
-                                           : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
-                                                 sizeof(uint32_t);
-    const size_t lds = n_att * 3 * sizeof(float) + stack_bytes;
-    launch_trace(dc->kinds, dc->has_plane, small_depth, dim3(blocks), lds, c->stream, ks, kc, kp, c->d_mean,
-                 c->d_u8, c->d_cnt);
+  const uint32_t sum_blocks = (kp.P + 255u) / 256u;
+  int traced = 0;  // trace launches whose events were recorded
+  for (int pass = 0; pass < passes || (pass == 0 && kp.P); ++pass) {
+    kp.b0 = static_cast<uint32_t>(pass) * nb_pass;
+    kp.nb = pass < passes ? min(nb_pass, nblocks - kp.b0) : 0u;
+    kp.n_items = static_cast<uint64_t>(kp.nb) * kp.P;
+    if (kp.n_items) {
+      // persistent grid: enough waves to fill every CU (extra blocks find the queue empty)
+      const uint64_t want = (kp.n_items + 255u) / 256u;
+      const uint32_t blocks = static_cast<uint32_t>(want < 8ull * c->num_cus ? want : 8ull * c->num_cus);
+      HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(unsigned long long), c->stream));
+      HIPCHK(hipEventRecord(c->ev_trace[2 * traced], c->stream));
+      launch_trace(dc->kinds, dc->has_plane, small_depth, dim3(blocks), lds, c->stream, ks, kc, kp, kw);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(c->ev_trace[2 * traced + 1], c->stream));
+      ++traced;
+    }
+    const int first = pass == 0, last = pass + 1 >= passes;
+    hipLaunchKernelGGL(sum_kernel, dim3(sum_blocks ? sum_blocks : 1u), dim3(256), 0, c->stream, kp, c->d_samples,
+                       c->d_running, c->d_mean, c->d_u8, first, last);
     HIPCHK(hipGetLastError());
+    if (last) break;
   }
+  c->passes = traced;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   c->last = *p;
   c->last_n = dc->n;
@@ -793,6 +970,14 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
             cnt[4 + DG_ITER], cnt[4 + DG_REGEN_W], cnt[4 + DG_REGEN_L], cnt[4 + DG_HIT_W], cnt[4 + DG_END_W],
             cnt[4 + DG_END_L], cnt[4 + DG_UNW_W], cnt[4 + DG_UNW_L], dl[0], dl[1], dr[0], dr[1], cnt[4 + DG_LENS_W],
             cnt[4 + DG_LENS_L], cnt[0], cnt[1]);
+    if (const char* path = getenv("FR_DIAG_TIMES")) {
+      std::vector<unsigned long long> wt(2 * 65536);
+      HIPCHK(hipMemcpyFromSymbol(wt.data(), HIP_SYMBOL(g_fr_wave_times), wt.size() * 8));
+      if (FILE* f = fopen(path, "wb")) {
+        fwrite(wt.data(), 8, wt.size(), f);
+        fclose(f);
+      }
+    }
 #endif
     float ms = 0.0f;
     HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
@@ -808,6 +993,13 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
     st->samples = rows * p.width * static_cast<uint64_t>(p.spp);
     st->prim_tests = cnt[0] * static_cast<uint64_t>(c->last_n);
     st->kernel_ms = ms;
+    double tms = 0.0;
+    for (int i = 0; i < c->passes; ++i) {
+      float t = 0.0f;
+      HIPCHK(hipEventElapsedTime(&t, c->ev_trace[2 * i], c->ev_trace[2 * i + 1]));
+      tms += t;
+    }
+    st->trace_ms = tms;
     st->total_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t0).count();
   }
@@ -909,6 +1101,7 @@ int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* 
       stats->samples += sts[g].samples;
       stats->prim_tests += sts[g].prim_tests;
       if (sts[g].kernel_ms > stats->kernel_ms) stats->kernel_ms = sts[g].kernel_ms;
+      if (sts[g].trace_ms > stats->trace_ms) stats->trace_ms = sts[g].trace_ms;
     }
     stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }

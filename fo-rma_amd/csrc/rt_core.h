@@ -65,12 +65,11 @@ FR_HD float schlick(float cosine, float ref_idx) {
 }
 
 // ---------------------------------------------------------------------------
-// RNG. One stream per (seed, pixel): splitmix64 keys a xoshiro128+ 1.0 state
-// (Blackman & Vigna's generator for floating-point output: only the upper bits are
-// used); the pixel's samples draw from it in sample order, as the reference's
-// save_image draws every sample from one sequential stream (tracer.rs:164-175).
-// f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits). `stream` selects independent
-// streams of one pixel (0 for rendering; the self-tests use others).
+// RNG. One stream per (seed, pixel, block of 16 samples): splitmix64 keys a
+// xoshiro128+ 1.0 state (Blackman & Vigna's generator for floating-point output:
+// only the upper bits are used); a block's samples draw from it in sample order (the
+// reference's save_image draws every sample from one sequential stream,
+// tracer.rs:164-175). f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits).
 // ---------------------------------------------------------------------------
 struct Rng {
   uint32_t s0, s1, s2, s3;
@@ -84,8 +83,8 @@ FR_HD uint64_t splitmix64_next(uint64_t& x) {
   return z ^ (z >> 31);
 }
 
-FR_HD Rng rng_seed(uint64_t seed, uint32_t pixel, uint32_t stream) {
-  uint64_t x = seed ^ ((static_cast<uint64_t>(pixel) << 32) | static_cast<uint64_t>(stream));
+FR_HD Rng rng_seed(uint64_t seed, uint32_t pixel, uint32_t block) {
+  uint64_t x = seed ^ ((static_cast<uint64_t>(pixel) << 32) | static_cast<uint64_t>(block));
   uint64_t a = splitmix64_next(x);
   uint64_t b = splitmix64_next(x);
   return Rng{static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),

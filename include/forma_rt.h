@@ -110,7 +110,8 @@ typedef struct fr_camera {
  * Render parameters. Rows are grouped into strips of `strip_rows` (must be 8) rows;
  * strip k belongs to shard (k % shard_count). A shard renders only its own strips,
  * so shards of one image are disjoint and stitch bit-exactly.
- * RNG: one counter-based stream per (seed, global pixel index y*W+x, sample index).
+ * RNG: one stream per (seed, global pixel index y*W+x, block of 16 samples); a block's
+ * samples draw from it in order.
  */
 typedef struct fr_params {
   uint32_t width, height;
@@ -128,8 +129,9 @@ typedef struct fr_stats {
   uint64_t hits;       /* segments whose closest-hit loop found an object */
   uint64_t samples;    /* paths started = pixels * spp */
   uint64_t prim_tests; /* segments * n_prims */
-  double kernel_ms;    /* HIP-event time of the trace kernel on its stream */
+  double kernel_ms;    /* HIP-event time of the whole render on its stream (all kernels) */
   double total_ms;     /* host wall time of the call */
+  double trace_ms;     /* HIP-event time of the trace kernel(s) alone */
 } fr_stats;
 
 typedef struct fr_scene fr_scene; /* opaque: host primitive list + per-device copies */

@@ -75,9 +75,9 @@ struct ReflectRecord {
 
 // ---- the RNG that replaces rand::thread_rng() -------------------------------
 // splitmix64 (Steele, Lea & Flood 2014) keys xoshiro128+ 1.0 (Blackman & Vigna
-// 2018) per (seed, pixel, stream); rendering uses stream 0 of each pixel and draws
-// the pixel's samples from it in order, like save_image's one sequential ThreadRng
-// (tracer.rs:164-175); f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits).
+// 2018) per (seed, pixel, stream); sample s of a pixel draws from stream s / 16, the
+// 16 samples of a block in order (the reference's save_image draws every sample from
+// one sequential ThreadRng, tracer.rs:164-175); f32 = ((u32 ^ 2^31) >> 8) * 2^-24.
 struct Rng {
   uint32_t s[4];
   static uint64_t splitmix(uint64_t& x) {
@@ -707,8 +707,10 @@ int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, ui
       for (uint32_t x = 0; x < width; ++x) {
         const uint32_t pixel = y * width + x;
         Vec3 col = Vec3::zero();
-        Rng rng(seed, pixel, 0);  // the pixel's stream; samples draw from it in order
+        Rng rng(seed, pixel, 0);
         for (uint32_t s = 0; s < spp; ++s) {
+          // samples come in blocks of 16; block b draws from stream (seed, pixel, b) in order
+          if (s % 16 == 0) rng = Rng(seed, pixel, s / 16);
           const float u = (float(x) + rng.gen_f32()) / float(width);
           const float v = (float(height - y) + rng.gen_f32()) / float(height);
           const Ray ray = camera.get_ray(u, v, rng);

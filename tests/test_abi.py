@@ -27,7 +27,7 @@ def test_abi_version_and_struct_sizes(fr):
     assert C.sizeof(fr.FrPrim) == 88
     assert C.sizeof(fr.FrCamera) == 26 * 4
     assert C.sizeof(fr.FrParams) == 40  # static_assert-ed in render.hip
-    assert C.sizeof(fr.FrStats) == 48
+    assert C.sizeof(fr.FrStats) == 56
 
 
 def test_library_links_the_gfx950_code_object():

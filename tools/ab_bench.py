@@ -17,10 +17,10 @@ CHILD = r'''
 import json, os, sys, hashlib
 sys.path.insert(0, os.path.join(sys.argv[1], "fo-rma_amd"))
 import forma_rt as fr
-scene, w, h, spp, depth, steps = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6]), int(sys.argv[7])
+scene, w, h, spp, depth, steps, shards = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6]), int(sys.argv[7]), int(sys.argv[8])
 sc = fr.Scene.from_file(fr.scene_path(scene), w, h)
 ctx = fr.RenderContext(0)
-p = fr.make_params(w, h, spp, depth)
+p = fr.make_params(w, h, spp, depth, shard_index=0, shard_count=shards)
 ctx.render(sc, sc.camera, p); ctx.sync()
 ms = []
 for _ in range(steps):
@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--size", default="1920x1080")
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--shards", type=int, default=1, help="time shard 0 of this many (one rank of N GPUs)")
     a = ap.parse_args()
     w, h = map(int, a.size.split("x"))
     res = {lib: [] for lib in a.libs}
@@ -47,7 +48,7 @@ def main():
         for lib in a.libs:
             env = dict(os.environ, FORMA_RT_LIB=os.path.abspath(lib))
             out = subprocess.run([sys.executable, "-c", CHILD, ROOT, a.scene, str(w), str(h), str(a.spp),
-                                  str(a.depth), str(a.steps)], env=env, capture_output=True, text=True, timeout=300)
+                                  str(a.depth), str(a.steps), str(a.shards)], env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(lib, "FAILED", out.stderr[-2000:])
                 sys.exit(1)
@@ -57,7 +58,7 @@ def main():
     base = shas[a.libs[0]]
     for lib in a.libs:
         ms = sorted(res[lib])[len(res[lib]) // 2]
-        samples = w * h * a.spp
+        samples = w * h * a.spp / a.shards
         print(f"{os.path.basename(lib):32s} {ms:9.3f} ms  {samples / ms / 1e3:10.1f} Msamples/s  "
               f"{'same image' if shas[lib] == base else 'IMAGE DIFFERS ' + shas[lib]}")
 
