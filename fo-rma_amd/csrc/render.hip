@@ -60,7 +60,7 @@ constexpr uint32_t kMaxDepth = 64;    // LDS stack bound (64 KB per workgroup)
 #endif
 constexpr uint32_t kSmallDepth = 8;
 constexpr uint32_t kBlockSamples = 16;  // samples per RNG stream (numerics contract)
-constexpr uint64_t kBatch = 64;         // work items claimed per global atomic (one tile, one block)  // max_depth <= 8: u16 index stack, unrolled unwind
+constexpr uint32_t kBatch = 64;         // work items claimed per global atomic (one tile, one block)  // max_depth <= 8: u16 index stack, unrolled unwind
 
 // ABI layout, mirrored by ctypes (forma_rt.py) and the Rust binding
 static_assert(sizeof(fr_prim) == 88, "fr_prim layout");
@@ -100,12 +100,32 @@ struct KParams {
   uint32_t shard_index, shard_count, tiles_per_row, n_tiles, flags;
   uint32_t P;         // pixel slots of the shard: n_tiles x 64, tile order
   uint32_t b0, nb;    // this pass renders sample blocks [b0, b0 + nb)
-  uint64_t n_items;   // nb x P work items (pixel slot, block)
+  uint32_t n_items;   // nb x P work items (pixel slot, block); < 2^32 per pass
+  uint32_t tiles_magic, tiles_shift;  // x / n_tiles = fastdiv(x, tiles_magic, tiles_shift)
 };
+
+// Unsigned 32-bit division by the invariant n_tiles: q = (t + ((x - t) >> s1)) >> s2 with
+// t = mulhi(x, m), l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1, s1 = min(l, 1),
+// s2 = max(l - 1, 0) (Granlund-Montgomery; d = 1 gives m = 1, q = x). tests/test_fastdiv.py.
+__host__ __device__ __forceinline__ uint32_t fastdiv(uint32_t x, uint32_t m, uint32_t shifts) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t t = __umulhi(x, m);
+#else
+  const uint32_t t = static_cast<uint32_t>((static_cast<uint64_t>(x) * m) >> 32);
+#endif
+  return (t + ((x - t) >> (shifts & 1u))) >> (shifts >> 1);
+}
+
+static void fastdiv_magic(uint32_t d, uint32_t& m, uint32_t& shifts) {
+  if (d < 1) d = 1;
+  const uint32_t l = d == 1 ? 0u : 32u - static_cast<uint32_t>(__builtin_clz(d - 1));
+  m = static_cast<uint32_t>(((static_cast<uint64_t>(1) << 32) * ((static_cast<uint64_t>(1) << l) - d)) / d + 1);
+  shifts = (l < 1 ? l : 1u) | ((l > 0 ? l - 1 : 0u) << 1);
+}
 
 // Work buffers of one render pass.
 struct KWork {
-  unsigned long long* queue;  // next unclaimed item (zeroed before the pass)
+  uint32_t* queue;            // next unclaimed item (zeroed before the pass)
   float* samples;             // per-sample colours, [(s - 16*b0) * P + q] x 3 f32
   unsigned long long* counters;
 };
@@ -218,7 +238,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     KScene sc, KCam cam, KParams kp, KWork kw) {
   // LDS: [attenuation rgb, n_att entries][stack: MAXD ? MAXD x kBlock u16 : max_depth x kBlock u32]
   extern __shared__ uint32_t lds[];
-  __shared__ unsigned long long wq_next[kBlock / 64], wq_end[kBlock / 64];  // per-wave item batch
+  __shared__ uint32_t wq_next[kBlock / 64], wq_end[kBlock / 64];  // per-wave item batch
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
   float* att_lds = reinterpret_cast<float*>(lds);
   uint32_t* stack = lds + n_att * 3u;
@@ -250,9 +270,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 
   enum : uint32_t { NEED_NONE = 0, NEED_LENS = 1, NEED_SPHERE = 2 };
   uint32_t depth = 0;
-  auto att_of = [&](uint32_t pi) -> V3 {
-    return n_att ? V3{att_lds[3 * pi], att_lds[3 * pi + 1], att_lds[3 * pi + 2]} : xyz(sc.att[pi]);
-  };
   // stack push at level `depth` of the scatter winner
   auto push = [&](uint32_t pi) {
     if (MAXD > 0)
@@ -268,6 +285,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   float sfuzz = 0.0f, fx = 0.0f, fy = 0.0f;
   bool smetal = false;
   uint32_t sbest = 0, q = 0, s = 0, s_end = 0, nseg = 0, nhit = 0;
+  float* out = kw.samples;                               // colour slot of the current sample
+  const size_t out_stride = 3 * static_cast<size_t>(kp.P);  // next sample of the same pixel
   Rng rng{0u, 0u, 0u, 0u};
   bool active = true, need_item = true, have_ray = false;
   uint32_t need = NEED_NONE;
@@ -281,29 +300,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       const uint32_t n = static_cast<uint32_t>(__popcll(m));
       const uint32_t r = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-      const unsigned long long next = wq_next[wave], end = wq_end[wave];
-      const unsigned long long avail = end - next;
-      unsigned long long base = 0;
+      const uint32_t next = wq_next[wave], end = wq_end[wave];
+      const uint32_t avail = end - next;
+      uint32_t base = 0;
       if (n > avail) {
-        if (r == 0) base = atomicAdd(kw.queue, static_cast<unsigned long long>(kBatch));
+        if (r == 0) base = atomicAdd(kw.queue, static_cast<uint32_t>(kBatch));
         base = __builtin_amdgcn_readfirstlane(base);
       }
-      const unsigned long long item = r < avail ? next + r : base + (r - avail);
+      const uint32_t item = r < avail ? next + r : base + (r - avail);
       if (r == 0) {
         wq_next[wave] = n > avail ? base + (n - avail) : next + n;
-        if (n > avail) wq_end[wave] = base + kBatch;
+        if (n > avail) wq_end[wave] = base + static_cast<uint32_t>(kBatch);
       }
       if (item >= kp.n_items) {
         active = false;  // queue drained
         continue;
       }
-      const uint32_t b = kp.b0 + static_cast<uint32_t>(item / kp.P);
-      q = static_cast<uint32_t>(item % kp.P);
+      // item = (b - b0) * P + q with P = 64 * n_tiles: split via the tile-block index
+      const uint32_t tb = item >> 6;
+      const uint32_t bl = fastdiv(tb, kp.tiles_magic, kp.tiles_shift);
+      const uint32_t b = kp.b0 + bl;
+      q = ((tb - bl * kp.n_tiles) << 6) | (item & 63u);
       uint32_t x, y;
       if (slot_xy(kp, q, x, y)) {
         const uint32_t pixel = y * kp.W + x;
         rng = rng_seed(kp.seed, pixel, b);  // this block's stream
         s = b * kBlockSamples;
+        out = kw.samples + 3 * (static_cast<size_t>(s - s_pass) * kp.P + q);
         s_end = min(s + kBlockSamples, kp.spp);
         fx = static_cast<float>(x);
         fy = static_cast<float>(kp.H - y);  // tracer.rs:171-172
@@ -464,26 +487,34 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       DIAG_WAVE(DG_END_W);
       DIAG_LANE(DG_END_L);
       V3 col = term;
-      if (MAXD > 0) {
+      // n_att is wave-uniform: one unwind per attenuation source keeps LDS reads as
+      // ds_read (a merged pointer would become flat loads)
+      if (MAXD > 0 && n_att) {
 #pragma unroll
         for (int j = MAXD - 1; j >= 0; --j) {
           if (j < static_cast<int>(depth)) {
             DIAG_WAVE(DG_UNW_W);
             DIAG_LANE(DG_UNW_L);
-            col = mul(att_of(hstack[j * kBlock + tid]), col);
+            const uint32_t pi = hstack[j * kBlock + tid];
+            col = mul(V3{att_lds[3 * pi], att_lds[3 * pi + 1], att_lds[3 * pi + 2]}, col);
           }
         }
-      } else {
+      } else if (MAXD > 0) {
+#pragma unroll
+        for (int j = MAXD - 1; j >= 0; --j)
+          if (j < static_cast<int>(depth)) col = mul(xyz(sc.att[hstack[j * kBlock + tid]]), col);
+      } else if (n_att) {
         for (int j = static_cast<int>(depth) - 1; j >= 0; --j) {
-          DIAG_WAVE(DG_UNW_W);
-          DIAG_LANE(DG_UNW_L);
-          col = mul(att_of(stack[j * kBlock + tid]), col);
+          const uint32_t pi = stack[j * kBlock + tid];
+          col = mul(V3{att_lds[3 * pi], att_lds[3 * pi + 1], att_lds[3 * pi + 2]}, col);
         }
+      } else {
+        for (int j = static_cast<int>(depth) - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
       }
-      float* out = kw.samples + 3 * (static_cast<size_t>(s - s_pass) * kp.P + q);
       out[0] = col.x;
       out[1] = col.y;
       out[2] = col.z;
+      out += out_stride;
       if (++s == s_end) {
         need_item = true;
       } else {
@@ -872,10 +903,16 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
       strips > p->shard_index ? (strips - p->shard_index + p->shard_count - 1) / p->shard_count : 0u;
   kp.n_tiles = my_strips * kp.tiles_per_row;
   kp.P = kp.n_tiles * 64u;
+  fastdiv_magic(kp.n_tiles, kp.tiles_magic, kp.tiles_shift);
   const uint32_t nblocks = (p->spp + kBlockSamples - 1) / kBlockSamples;
   // passes: as many sample blocks per pass as the sample buffer holds
   const size_t per_block = static_cast<size_t>(kp.P) * kBlockSamples * 3 * sizeof(float);
   uint32_t nb_pass = per_block ? static_cast<uint32_t>(sample_buffer_cap() / per_block) : nblocks;
+  // 32-bit item indices. After the queue drains, every wave may still bump the counter
+  // once per lane (each claim retires >= 1 lane): <= 8 blocks/CU x 4 waves x 64 x 64 on
+  // 256 CUs = 2^25 past n_items, so keep 2^28 of headroom below 2^32.
+  constexpr uint32_t kItemLimit = 0xFFFFFFFFu - (1u << 28);
+  if (kp.P && nb_pass > kItemLimit / kp.P) nb_pass = kItemLimit / kp.P;
   if (nb_pass < 1) nb_pass = 1;
   if (nb_pass > nblocks) nb_pass = nblocks;
   const int passes = nblocks ? static_cast<int>((nblocks + nb_pass - 1) / nb_pass) : 0;
@@ -906,7 +943,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
                                                sizeof(uint32_t);
   const size_t lds = n_att * 3 * sizeof(float) + stack_bytes;
   KWork kw;
-  kw.queue = c->d_cnt + 31;
+  kw.queue = reinterpret_cast<uint32_t*>(c->d_cnt + 31);
   kw.samples = c->d_samples;
   kw.counters = c->d_cnt;
   c->t0 = std::chrono::steady_clock::now();
@@ -924,12 +961,12 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   for (int pass = 0; pass < passes || (pass == 0 && kp.P); ++pass) {
     kp.b0 = static_cast<uint32_t>(pass) * nb_pass;
     kp.nb = pass < passes ? min(nb_pass, nblocks - kp.b0) : 0u;
-    kp.n_items = static_cast<uint64_t>(kp.nb) * kp.P;
+    kp.n_items = kp.nb * kp.P;
     if (kp.n_items) {
       // persistent grid: enough waves to fill every CU (extra blocks find the queue empty)
-      const uint64_t want = (kp.n_items + 255u) / 256u;
+      const uint64_t want = (static_cast<uint64_t>(kp.n_items) + 255u) / 256u;
       const uint32_t blocks = static_cast<uint32_t>(want < 8ull * c->num_cus ? want : 8ull * c->num_cus);
-      HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(unsigned long long), c->stream));
+      HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), c->stream));
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced], c->stream));
       launch_trace(dc->kinds, dc->has_plane, small_depth, dim3(blocks), lds, c->stream, ks, kc, kp, kw);
       HIPCHK(hipGetLastError());
