@@ -102,6 +102,7 @@ struct KParams {
   uint32_t b0, nb;    // this pass renders sample blocks [b0, b0 + nb)
   uint32_t n_items;   // nb x P work items (pixel slot, block); < 2^32 per pass
   uint32_t tiles_magic, tiles_shift;  // x / n_tiles = fastdiv(x, tiles_magic, tiles_shift)
+  float rW, rH;                       // RN(1 / W), RN(1 / H) (host IEEE division)
 };
 
 // Unsigned 32-bit division by the invariant n_tiles: q = (t + ((x - t) >> s1)) >> s2 with
@@ -333,8 +334,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         // first sample of the block: jitter; the lens sample follows in step 1
         const float r0 = rng_f32(rng);
         const float r1 = rng_f32(rng);
-        d.x = (fx + r0) / fW;
-        d.y = (fy + r1) / fH;
+        d.x = div_rn(fx + r0, fW, kp.rW);  // (fx + r0) / fW, numerator +0 or in [2^-24, 2^32]
+        d.y = div_rn(fy + r1, fH, kp.rH);
         need = NEED_LENS;
         need_item = false;
       }
@@ -392,7 +393,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       // 2. closest hit over the list in order (tracer.rs:190-200): only the accepted t
       // of each test is needed here; the record is formed for the winner below.
       ++nseg;
-      const V3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+      V3 inv{recip_nr(d.x), recip_nr(d.y), recip_nr(d.z)};
+      if (!(recip_nr_ok(d.x) && recip_nr_ok(d.y) && recip_nr_ok(d.z))) inv = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
       const float a_dd = dot(d, d);
       float closest = FLT_MAX, t_last = 0.0f;
       int best = -1;
@@ -521,8 +523,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         // next sample of the block: jitter (tracer.rs:171-172), same stream
         const float r0 = rng_f32(rng);
         const float r1 = rng_f32(rng);
-        d.x = (fx + r0) / fW;
-        d.y = (fy + r1) / fH;
+        d.x = div_rn(fx + r0, fW, kp.rW);
+        d.y = div_rn(fy + r1, fH, kp.rH);
         need = NEED_LENS;
       }
     }
@@ -597,9 +599,29 @@ __global__ void ops_kernel(int op, const float* a, const float* b, uint32_t n, f
     case 6: r = static_cast<float>(to_u8(x)); break;
     case 7: r = unit(V3{x, y, 1.0f}).x; break;
     case 8: r = 1.0f / x; break;
+    case 9: r = div_rn(x, y, 1.0f / y); break;  // the kernel's jitter division
+    case 10: r = recip_nr_ok(x) ? recip_nr(x) : 1.0f / x; break;
     default: r = 0.0f;
   }
   out[i] = r;
+}
+
+// Exhaustive check of recip_nr (rcp + one FMA Newton step) against the correctly
+// rounded 1.0f / x over x = [base, base + count): per exponent field (256 buckets) the
+// number of results whose bits differ (NaN == NaN) and the first such input.
+__global__ void recip_check_kernel(uint64_t base, uint64_t count, unsigned long long* bad, uint32_t* first) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < count; i += stride) {
+    const uint32_t bits = static_cast<uint32_t>(base + i);
+    const float x = __uint_as_float(bits);
+    const float want = 1.0f / x, got = recip_nr(x);
+    const bool same = __float_as_uint(want) == __float_as_uint(got) || (want != want && got != got);
+    if (!same) {
+      const uint32_t e = (bits >> 23) & 0xFFu;
+      atomicAdd(&bad[e], 1ull);
+      atomicMin(&first[e], bits);
+    }
+  }
 }
 
 __global__ void rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
@@ -891,6 +913,8 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   KParams kp;
   kp.W = p->width;
   kp.H = p->height;
+  kp.rW = 1.0f / static_cast<float>(p->width);
+  kp.rH = 1.0f / static_cast<float>(p->height);
   kp.spp = p->spp;
   kp.max_depth = p->max_depth;
   kp.seed = p->seed;
@@ -1173,6 +1197,26 @@ int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, 
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(out, d, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIPCHK(hipFree(d));
+  return FR_OK;
+}
+
+/* Diagnostic: exhaustive recip_nr check over [base, base + count) bit patterns;
+   bad[256] / first[256] per exponent field (first = 0xFFFFFFFF when none). */
+int fr_selftest_recip(int device, uint64_t base, uint64_t count, uint64_t* bad, uint32_t* first) {
+  if (!bad || !first || base + count > (1ull << 32)) return set_error(FR_EARG, "fr_selftest_recip: bad arguments");
+  HIPCHK(hipSetDevice(device));
+  unsigned long long* dbad = nullptr;
+  uint32_t* dfirst = nullptr;
+  HIPCHK(hipMalloc(&dbad, 256 * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&dfirst, 256 * sizeof(uint32_t)));
+  HIPCHK(hipMemset(dbad, 0, 256 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(dfirst, 0xFF, 256 * sizeof(uint32_t)));
+  if (count) hipLaunchKernelGGL(recip_check_kernel, dim3(8192), dim3(256), 0, 0, base, count, dbad, dfirst);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(bad, dbad, 256 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(first, dfirst, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(dbad));
+  HIPCHK(hipFree(dfirst));
   return FR_OK;
 }
 

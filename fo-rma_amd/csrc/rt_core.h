@@ -206,6 +206,41 @@ FR_HD float fmax_num(float a, float b) {
 #endif
 }
 
+#if defined(__HIP__)
+// v_rcp_f32 (1 ulp) refined by one FMA Newton step: r' = r + r (1 - x r). Equal to the
+// correctly rounded 1.0f / x for every x whose exponent field is in [kRecipExpLo,
+// kRecipExpHi] (exhaustively checked on the device: fr_selftest_recip,
+// tests/test_gpu_parity.py::test_recip_nr_exhaustive); callers take 1.0f / x elsewhere.
+__device__ __forceinline__ float recip_nr(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float r = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, r, 1.0f);
+  return __builtin_fmaf(e, r, r);
+#else
+  return 1.0f / x;  // not used on the host
+#endif
+}
+
+// Reciprocal as the parity contract needs it (correctly rounded): recip_nr inside its
+// exhaustively checked range, the full IEEE division otherwise (zero, denormals,
+// |x| >= 2^126, inf, NaN). The fallback is a real branch, skipped by waves with no such lane.
+__device__ __forceinline__ bool recip_nr_ok(float x) {
+  const float ax = __builtin_fabsf(x);
+  return (ax >= 0x1p-126f) & (ax < 0x1p126f);
+}
+
+// a / b correctly rounded, given y = RN(1 / b): the compiler's own IEEE f32 division
+// sequence (y, q0 = a y, two FMA residual corrections) without its v_div_scale /
+// v_div_fmas / v_div_fixup steps, which are identities when a = +0 or |a| in
+// [2^-100, 2^100] and |b| in [2^-100, 2^100] (no operand or quotient near the
+// denormal / overflow range). Used only where the operand ranges hold by construction.
+__device__ __forceinline__ float div_rn(float a, float b, float y) {
+  const float q0 = a * y;
+  const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
+  return __builtin_fmaf(__builtin_fmaf(-b, q1, a), y, q1);
+}
+#endif
+
 struct Slab {
   V3 t0, t1;  // slab distances per axis
   float tn, tf;

@@ -79,7 +79,7 @@ EXPORTS = (
     "fr_scene_get_prims", "fr_scene_translate", "fr_scene_rotate",
     "fr_camera_init", "fr_camera_look", "fr_camera_orbit", "fr_camera_translate", "fr_update_delta",
     "fr_ctx_create", "fr_ctx_free", "fr_ctx_render", "fr_ctx_sync", "fr_ctx_download", "fr_ctx_device_buffers",
-    "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng",
+    "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_recip",
 )
 
 _lib = None
@@ -135,6 +135,8 @@ def lib():
     L.fr_render_hip_multi.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
     L.fr_selftest_ops.argtypes = [C.c_int, C.c_int, f3, f3, C.c_uint32, f3]
     L.fr_selftest_rng.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+    if hasattr(L, "fr_selftest_recip"):  # absent from A/B builds of older sources
+        L.fr_selftest_recip.argtypes = [C.c_int, C.c_uint64, C.c_uint64, P(C.c_uint64), P(C.c_uint32)]
     _lib = L
     return L
 

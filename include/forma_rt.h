@@ -189,6 +189,10 @@ int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* 
    parity tests to show the GPU arithmetic is bit-identical to the host's. */
 int fr_selftest_ops(int device, int op, const float* a, const float* b, uint32_t n, float* out);
 int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out);
+/* Compare the device's fast reciprocal (rcp + one Newton step) with the correctly rounded
+   1.0f / x for every f32 bit pattern in [base, base + count): mismatches per exponent
+   field in bad[256], first mismatching pattern in first[256] (0xFFFFFFFF = none). */
+int fr_selftest_recip(int device, uint64_t base, uint64_t count, uint64_t* bad, uint32_t* first);
 
 #ifdef __cplusplus
 }

@@ -65,6 +65,48 @@ def test_device_arithmetic_is_ieee_correctly_rounded(gpu, op):
     assert _same_bits(out, want.astype(np.float32))
 
 
+def test_recip_nr_exhaustive(gpu):
+    """rcp + one FMA Newton step equals the correctly rounded 1.0f / x for every f32 whose
+    exponent field is 1..252; the kernel's guard (recip_nr_ok) sends all others, and only
+    those, to the IEEE division. All 2^32 bit patterns are checked on the device."""
+    import ctypes as C
+    bad = np.zeros(256, np.uint64)
+    first = np.zeros(256, np.uint32)
+    gpu.check(gpu.lib().fr_selftest_recip(0, 0, 1 << 32, bad.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                          first.ctypes.data_as(C.POINTER(C.c_uint32))))
+    assert not bad[1:253].any(), {e: (int(bad[e]), hex(int(first[e]))) for e in np.nonzero(bad[1:253])[0] + 1}
+
+
+def test_guarded_recip_and_jitter_division(gpu):
+    """The kernel's fast reciprocal with its range guard (op 10) and its jitter division
+    div_rn((x + r) , W, RN(1/W)) (op 9) against numpy's IEEE float32 division."""
+    import ctypes as C
+    rng = np.random.default_rng(11)
+    fp = C.POINTER(C.c_float)
+    x = _edge_floats(rng, 200000)
+    tiny = np.array([1e-38, -1e-38, 2.0 ** -126, -(2.0 ** -126), 2.0 ** -127, 2.0 ** 126, 2.0 ** 127, 3e38, -3e38,
+                     0.0, -0.0, 1e-45], dtype=np.float32)
+    x = np.concatenate([x, tiny])
+    out = np.empty_like(x)
+    gpu.check(gpu.lib().fr_selftest_ops(0, 10, x.ctypes.data_as(fp), x.ctypes.data_as(fp), x.size,
+                                        out.ctypes.data_as(fp)))
+    with np.errstate(all="ignore"):
+        assert _same_bits(out, np.float32(1.0) / x)
+    for wh in (1, 3, 7, 64, 255, 256, 270, 480, 1080, 1920, 2160, 3840, 4097, 65535, 100003):
+        fx = rng.integers(0, wh + 1, 300000).astype(np.float32)
+        r = (rng.integers(0, 1 << 24, fx.size).astype(np.float64) * 2.0 ** -24).astype(np.float32)
+        r[:64] = np.float32(0.0)
+        r[64:128] = np.float32(2.0 ** -24)
+        r[128:192] = np.float32(1.0 - 2.0 ** -24)
+        fx[:192] = np.tile(np.array([0, 1, wh - 1 if wh > 1 else 0, wh], np.float32), 48)
+        a = (fx + r).astype(np.float32)
+        b = np.full_like(a, np.float32(wh))
+        out = np.empty_like(a)
+        gpu.check(gpu.lib().fr_selftest_ops(0, 9, a.ctypes.data_as(fp), b.ctypes.data_as(fp), a.size,
+                                            out.ctypes.data_as(fp)))
+        assert _same_bits(out, a / b), wh
+
+
 def test_device_schlick_unit_and_u8_match_oracle(gpu):
     import ctypes as C
     rng = np.random.default_rng(2)

@@ -1,7 +1,16 @@
-import os, sys
+"""Run an FR_DIAG build (FORMA_RT_LIB=...) and print its phase counters.
+
+    python tools/diag_run.py [scene W H SPP] ...   (default: two small cases)"""
+import os
+import sys
 sys.path.insert(0, os.path.join(os.environ.get("GRAFT_REPO_ROOT", "/root/repo"), "fo-rma_amd"))
 import forma_rt as fr
-for scene, w, h, spp in [("scene_08", 480, 270, 64), ("scene_01", 480, 270, 16)]:
+
+cases = [("scene_08", 480, 270, 64), ("scene_01", 480, 270, 16)]
+if len(sys.argv) > 1:
+    a = sys.argv[1:]
+    cases = [(a[i], int(a[i + 1]), int(a[i + 2]), int(a[i + 3])) for i in range(0, len(a), 4)]
+for scene, w, h, spp in cases:
     sc = fr.Scene.from_file(fr.scene_path(scene), w, h)
     m, u, st = fr.render(sc, sc.camera, w, h, spp, 8)
-    print(scene, st, flush=True)
+    print(scene, w, h, spp, st, flush=True)
