@@ -248,18 +248,10 @@ struct Slab {
 
 FR_HD Slab slab3(V3 lo, V3 hi, V3 o, V3 inv) {
   Slab s;
-#if defined(__HIP_DEVICE_COMPILE__)
-  // same IEEE ops, two lanes per instruction (v_pk_add_f32 / v_pk_mul_f32)
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  const f2 oxy = {o.x, o.y}, ixy = {inv.x, inv.y};
-  const f2 a = (f2{lo.x, lo.y} - oxy) * ixy;
-  const f2 b = (f2{hi.x, hi.y} - oxy) * ixy;
-  s.t0 = V3{a.x, a.y, (lo.z - o.z) * inv.z};
-  s.t1 = V3{b.x, b.y, (hi.z - o.z) * inv.z};
-#else
+  // scalar f32 ops: packed v_pk_add/mul_f32 cost more issue time than two plain ops
+  // (MI355X_MICROARCH.md, "vector-instruction ISSUE cost"; measured -2% here)
   s.t0 = V3{(lo.x - o.x) * inv.x, (lo.y - o.y) * inv.y, (lo.z - o.z) * inv.z};
   s.t1 = V3{(hi.x - o.x) * inv.x, (hi.y - o.y) * inv.y, (hi.z - o.z) * inv.z};
-#endif
   s.tn = fmax_num(fmax_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y)), fmin_num(s.t0.z, s.t1.z));
   s.tf = fmin_num(fmin_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y)), fmax_num(s.t0.z, s.t1.z));
   return s;
