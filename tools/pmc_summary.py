@@ -1,5 +1,9 @@
 """Summarise a tools/profile.sh run: per-launch PMC values of trace_kernel and the
-kernel-trace statistics.   python tools/pmc_summary.py gpurun_out/prof/<tag>"""
+kernel-trace statistics.
+
+    python tools/pmc_summary.py gpurun_out/prof/<tag> [--write profiles/pmc_trace_kernel.json]
+
+--write stores the per-launch HBM bytes that bench.py reports as roofline.traffic."""
 import collections
 import csv
 import glob
@@ -26,6 +30,7 @@ def load(dirpath):
 
 def main():
     d = load(sys.argv[1])
+    hbm = None
     ns = d.get("avg_ns", 0)
     print(json.dumps(d, indent=1))
     if ns and "SQ_INSTS_VALU" in d:
@@ -36,6 +41,17 @@ def main():
         # gfx950: FETCH_SIZE (KB) counts 64 B per 128-B request: double it (MI355X_MICROARCH.md §HBM)
         hbm = (2 * d["FETCH_SIZE"] + d.get("WRITE_SIZE", 0)) * 1024
         print(f"HBM bytes/launch ~{hbm:.3e} ({hbm / (ns * 1e-9) / 1e9:.2f} GB/s)")
+    if "--write" in sys.argv and hbm is not None:
+        path = sys.argv[sys.argv.index("--write") + 1]
+        rec = {"workload": "scene_08 1920x1080 256spp d8", "kernel": "trace_kernel",
+               "hbm_bytes_per_launch": round(hbm), "fetch_size_kb": d["FETCH_SIZE"],
+               "write_size_kb": d.get("WRITE_SIZE"), "avg_ns": ns, "source": sys.argv[1],
+               "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE doubled "
+                       "(gfx950, MI355X_MICROARCH.md HBM section); WRITE_SIZE as reported (uncalibrated for "
+                       "12-B scattered stores)"}
+        with open(path, "w") as f:
+            json.dump(rec, f, indent=1)
+        print("wrote", path)
 
 
 if __name__ == "__main__":
