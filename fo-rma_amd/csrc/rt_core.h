@@ -12,7 +12,7 @@
 //   reflect/refract/schlick ... cpu_ray_tracer/utility.rs:27-54
 //   random_in_unit_{circle,sphere} ... utility.rs:4-25 (rejection loops)
 //   Rng ............... replaces rand::thread_rng() (rand 0.9.2, Cargo.lock:2735) with a
-//                       counter-keyed xoshiro128** stream per (seed, pixel, sample)
+//                       counter-keyed xoshiro128+ stream per (seed, pixel, 16-sample block)
 //   sphere_root ....... shapes/sphere.rs:23-51
 //   plane_test ........ shapes/plane.rs:24-44 (stale-record quirk kept)
 //   slab3/slab_root ... build-defined box, shaped like Sphere::hit
