@@ -103,6 +103,7 @@ struct KParams {
   uint32_t n_items;   // nb x P work items (pixel slot, block); < 2^32 per pass
   uint32_t tiles_magic, tiles_shift;  // x / n_tiles = fastdiv(x, tiles_magic, tiles_shift)
   float rW, rH;                       // RN(1 / W), RN(1 / H) (host IEEE division)
+  uint32_t row_magic, row_shift;      // x / tiles_per_row = fastdiv(x, row_magic, row_shift)
 };
 
 // Unsigned 32-bit division by the invariant n_tiles: q = (t + ((x - t) >> s1)) >> s2 with
@@ -198,12 +199,23 @@ __device__ __forceinline__ uint32_t lanes_set(bool b) { return static_cast<uint3
 // past the image edge are invalid.
 __device__ __forceinline__ bool slot_xy(const KParams& kp, uint32_t q, uint32_t& x, uint32_t& y) {
   const uint32_t tile = q >> 6, l = q & 63u;
-  const uint32_t ls = tile / kp.tiles_per_row;
+  const uint32_t ls = fastdiv(tile, kp.row_magic, kp.row_shift);  // tile / tiles_per_row
   const uint32_t tc = tile - ls * kp.tiles_per_row;
   const uint32_t strip = kp.shard_index + ls * kp.shard_count;
   x = tc * 8u + (l & 7u);
   y = strip * kStripRows + (l >> 3);
   return x < kp.W && y < kp.H;
+}
+
+// Work item -> (block b, pixel slot q, image x, y); false for a slot past the image edge.
+// item = (b - b0) * P + q with P = 64 * n_tiles: split via the tile-block index.
+__device__ __forceinline__ bool item_xy(const KParams& kp, uint32_t item, uint32_t& b, uint32_t& q, uint32_t& x,
+                                        uint32_t& y) {
+  const uint32_t tb = item >> 6;
+  const uint32_t bl = fastdiv(tb, kp.tiles_magic, kp.tiles_shift);
+  b = kp.b0 + bl;
+  q = ((tb - bl * kp.n_tiles) << 6) | (item & 63u);
+  return slot_xy(kp, q, x, y);
 }
 
 // Persistent path-tracing kernel. Work item = (pixel slot q, sample block b): the
@@ -296,7 +308,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     DIAG_WAVE(DG_ITER);
     if (need_item) {
       // 0. claim a work item: the free lanes take consecutive items of the wave's
-      // batch; when it runs out, the first free lane claims the next 64 globally
+      // batch; when it runs out, the first free lane claims the next 64 globally.
+      // (Prefetching the next item in batched refill passes measured slower.)
       const unsigned long long m = __ballot(1);
       const uint32_t n = static_cast<uint32_t>(__popcll(m));
       const uint32_t r = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
@@ -317,15 +330,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         active = false;  // queue drained
         continue;
       }
-      // item = (b - b0) * P + q with P = 64 * n_tiles: split via the tile-block index
-      const uint32_t tb = item >> 6;
-      const uint32_t bl = fastdiv(tb, kp.tiles_magic, kp.tiles_shift);
-      const uint32_t b = kp.b0 + bl;
-      q = ((tb - bl * kp.n_tiles) << 6) | (item & 63u);
-      uint32_t x, y;
-      if (slot_xy(kp, q, x, y)) {
-        const uint32_t pixel = y * kp.W + x;
-        rng = rng_seed(kp.seed, pixel, b);  // this block's stream
+      uint32_t b, x, y;
+      if (item_xy(kp, item, b, q, x, y)) {
+        rng = rng_seed(kp.seed, y * kp.W + x, b);  // this block's stream
         s = b * kBlockSamples;
         out = kw.samples + 3 * (static_cast<size_t>(s - s_pass) * kp.P + q);
         s_end = min(s + kBlockSamples, kp.spp);
@@ -601,6 +608,9 @@ __global__ void ops_kernel(int op, const float* a, const float* b, uint32_t n, f
     case 8: r = 1.0f / x; break;
     case 9: r = div_rn(x, y, 1.0f / y); break;  // the kernel's jitter division
     case 10: r = recip_nr_ok(x) ? recip_nr(x) : 1.0f / x; break;
+    case 11: r = fmax3_num(x, y, b[(i + 1) % n]); break;  // vs fmaxf(fmaxf(x, y), z)
+    case 12: r = fmin_num(fmin_num(x, y), b[(i + 1) % n]); break;
+    case 13: r = fmax_num(fmax_num(x, y), b[(i + 1) % n]); break;  // chained v_max_f32
     default: r = 0.0f;
   }
   out[i] = r;
@@ -928,6 +938,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   kp.n_tiles = my_strips * kp.tiles_per_row;
   kp.P = kp.n_tiles * 64u;
   fastdiv_magic(kp.n_tiles, kp.tiles_magic, kp.tiles_shift);
+  fastdiv_magic(kp.tiles_per_row, kp.row_magic, kp.row_shift);
   const uint32_t nblocks = (p->spp + kBlockSamples - 1) / kBlockSamples;
   // passes: as many sample blocks per pass as the sample buffer holds
   const size_t per_block = static_cast<size_t>(kp.P) * kBlockSamples * 3 * sizeof(float);

@@ -241,6 +241,18 @@ __device__ __forceinline__ float div_rn(float a, float b, float y) {
 }
 #endif
 
+// maxNum(maxNum(a, b), c) in one v_max3_f32 (same IEEE-mode NaN rule as the chained
+// v_max_f32; device-checked against fmaxf chains in test_device_max3_matches_fmaxf).
+FR_HD float fmax3_num(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return fmaxf(fmaxf(a, b), c);
+#endif
+}
+
 struct Slab {
   V3 t0, t1;  // slab distances per axis
   float tn, tf;
@@ -252,7 +264,7 @@ FR_HD Slab slab3(V3 lo, V3 hi, V3 o, V3 inv) {
   // (MI355X_MICROARCH.md, "vector-instruction ISSUE cost"; measured -2% here)
   s.t0 = V3{(lo.x - o.x) * inv.x, (lo.y - o.y) * inv.y, (lo.z - o.z) * inv.z};
   s.t1 = V3{(hi.x - o.x) * inv.x, (hi.y - o.y) * inv.y, (hi.z - o.z) * inv.z};
-  s.tn = fmax_num(fmax_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y)), fmin_num(s.t0.z, s.t1.z));
+  s.tn = fmax3_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y), fmin_num(s.t0.z, s.t1.z));
   s.tf = fmin_num(fmin_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y)), fmax_num(s.t0.z, s.t1.z));
   return s;
 }

@@ -77,6 +77,41 @@ def test_recip_nr_exhaustive(gpu):
     assert not bad[1:253].any(), {e: (int(bad[e]), hex(int(first[e]))) for e in np.nonzero(bad[1:253])[0] + 1}
 
 
+def test_device_max3_and_min3_match_fmaxf_fminf(gpu):
+    """The slab test's v_max3_f32 (tn) and the compiler's v_min3_f32 (tf) against the
+    host's fmaxf/fminf chains, bit for bit, on edge values (NaN, +-0, +-inf, denormals).
+    Slab distances come from arithmetic, which only makes quiet NaNs; signalling NaNs
+    (which IEEE-mode v_max quiets and propagates one step) are quieted for the host
+    comparison, and v_max3 must equal the chained v_max_f32 on them as on everything."""
+    import ctypes as C
+    rng = np.random.default_rng(12)
+    fp = C.POINTER(C.c_float)
+
+    def quiet(a):
+        u = a.view(np.uint32).copy()
+        snan = ((u & 0x7F800000) == 0x7F800000) & ((u & 0x007FFFFF) != 0)
+        u[snan] |= 0x00400000
+        return u.view(np.float32)
+
+    def run(op, x, y):
+        out = np.empty_like(x)
+        gpu.check(gpu.lib().fr_selftest_ops(0, op, x.ctypes.data_as(fp), y.ctypes.data_as(fp), x.size,
+                                            out.ctypes.data_as(fp)))
+        return out
+
+    x_raw = _edge_floats(rng, 50000)
+    y_raw = np.roll(_edge_floats(rng, 50000), 3)[: x_raw.size]
+    assert _same_bits(run(11, x_raw, y_raw), run(13, x_raw, y_raw))  # max3 == chained v_max, sNaN included
+    x, y = quiet(x_raw), quiet(y_raw)
+    z = np.roll(y, -1)
+    for op, f in ((11, np.fmax), (12, np.fmin)):
+        out = run(op, x, y)
+        want = f(f(x, y), z)
+        # fmaxf/fminf leave the sign of equal zeros unspecified; the slab test never depends on it
+        zero = (want == 0) & (out == 0)
+        assert _same_bits(out[~zero], want[~zero]), op
+
+
 def test_guarded_recip_and_jitter_division(gpu):
     """The kernel's fast reciprocal with its range guard (op 10) and its jitter division
     div_rn((x + r) , W, RN(1/W)) (op 9) against numpy's IEEE float32 division."""
