@@ -59,7 +59,10 @@ constexpr uint32_t kMaxDepth = 64;    // LDS stack bound (64 KB per workgroup)
 #define FR_NUM_SGPR 96
 #endif
 constexpr uint32_t kSmallDepth = 8;
-constexpr uint32_t kBlockSamples = 16;  // samples per RNG stream (numerics contract)
+#ifndef FR_BLOCK_SAMPLES
+#define FR_BLOCK_SAMPLES 16  // RNG contract: one stream per 16-sample block (oracle.cpp agrees)
+#endif
+constexpr uint32_t kBlockSamples = FR_BLOCK_SAMPLES;  // samples per RNG stream (numerics contract)
 constexpr uint32_t kBatch = 64;         // work items claimed per global atomic (one tile, one block)  // max_depth <= 8: u16 index stack, unrolled unwind
 
 // ABI layout, mirrored by ctypes (forma_rt.py) and the Rust binding
@@ -190,6 +193,21 @@ enum { DG_ITER, DG_REGEN_W, DG_REGEN_L, DG_LENS_W, DG_LENS_L, DG_RUS_W, DG_RUS_L
 #define DIAG_LANE(slot) do {} while (0)
 #endif
 
+// FR_PROF builds read the shader clock (s_memtime, wave-uniform) at the section
+// boundaries of the lane loop and add each wave's cycles per section into
+// counters[20 + k]: wall-clock residency by section. Never enabled in the product.
+#ifdef FR_PROF
+enum { PF_CLAIM, PF_REJ, PF_HIT, PF_SHADE, PF_END, PF_N };
+#define PROF_MARK(k)                                       \
+  do {                                                     \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
+    pf_acc[k] += t_ - pf_t;                                \
+    pf_t = t_;                                             \
+  } while (0)
+#else
+#define PROF_MARK(k) do {} while (0)
+#endif
+
 // HAS_PLANE: planes may leave the shared record's t/p stale (plane.rs:27-29), so
 // the last written t is tracked separately from the winner's.
 __device__ __forceinline__ uint32_t lanes_set(bool b) { return static_cast<uint32_t>(__popcll(__ballot(b))); }
@@ -301,9 +319,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   float* out = kw.samples;                               // colour slot of the current sample
   const size_t out_stride = 3 * static_cast<size_t>(kp.P);  // next sample of the same pixel
   Rng rng{0u, 0u, 0u, 0u};
-  bool active = true, need_item = true, have_ray = false;
+  bool active = true, need_item = true, need_jit = false, have_ray = false;
   uint32_t need = NEED_NONE;
 
+#ifdef FR_PROF
+  uint64_t pf_acc[PF_N] = {0, 0, 0, 0, 0};
+  uint64_t pf_t = __builtin_amdgcn_s_memtime();
+#endif
   while (active) {
     DIAG_WAVE(DG_ITER);
     if (need_item) {
@@ -338,15 +360,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         s_end = min(s + kBlockSamples, kp.spp);
         fx = static_cast<float>(x);
         fy = static_cast<float>(kp.H - y);  // tracer.rs:171-172
-        // first sample of the block: jitter; the lens sample follows in step 1
-        const float r0 = rng_f32(rng);
-        const float r1 = rng_f32(rng);
-        d.x = div_rn(fx + r0, fW, kp.rW);  // (fx + r0) / fW, numerator +0 or in [2^-24, 2^32]
-        d.y = div_rn(fy + r1, fH, kp.rH);
-        need = NEED_LENS;
+        need_jit = true;
         need_item = false;
       }
     }
+    if (need_jit) {
+      // a sample starts: jitter (tracer.rs:171-172), then its lens sample in step 1. One
+      // place for the first sample of a block and the next sample of the same block, so
+      // the wave runs it once per iteration
+      const float r0 = rng_f32(rng);
+      const float r1 = rng_f32(rng);
+      d.x = div_rn(fx + r0, fW, kp.rW);  // (fx + r0) / fW, numerator +0 or in [2^-24, 2^32]
+      d.y = div_rn(fy + r1, fH, kp.rH);
+      need = NEED_LENS;
+      need_jit = false;
+    }
+    PROF_MARK(PF_CLAIM);
     bool ended = false;
     V3 term{0.0f, 0.0f, 0.0f};
     if (need != NEED_NONE) {
@@ -396,6 +425,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         need = NEED_NONE;
       }
     }
+    PROF_MARK(PF_REJ);
     if (have_ray) {
       // 2. closest hit over the list in order (tracer.rs:190-200): only the accepted t
       // of each test is needed here; the record is formed for the winner below.
@@ -434,6 +464,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           if (HAS_PLANE) t_last = t;
         }
       }
+      PROF_MARK(PF_HIT);
       if (best < 0) {
         term = sky(d);  // tracer.rs:211-218
         ended = true;
@@ -491,6 +522,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         }
       }
     }
+    PROF_MARK(PF_SHADE);
     if (ended) {
       // 3. attenuation * get_color(...) (tracer.rs:206-207), innermost first
       DIAG_WAVE(DG_END_W);
@@ -524,17 +556,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       out[1] = col.y;
       out[2] = col.z;
       out += out_stride;
-      if (++s == s_end) {
+      if (++s == s_end)
         need_item = true;
-      } else {
-        // next sample of the block: jitter (tracer.rs:171-172), same stream
-        const float r0 = rng_f32(rng);
-        const float r1 = rng_f32(rng);
-        d.x = div_rn(fx + r0, fW, kp.rW);
-        d.y = div_rn(fy + r1, fH, kp.rH);
-        need = NEED_LENS;
-      }
+      else
+        need_jit = true;  // next sample of the block, same stream
     }
+    PROF_MARK(PF_END);
   }
 
   // per-wave counter reduction, one 64-bit atomic per wave per counter
@@ -547,6 +574,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     atomicAdd(&kw.counters[0], a);
     atomicAdd(&kw.counters[1], b);
   }
+#ifdef FR_PROF
+  if (lane == 0)
+    for (int k = 0; k < PF_N; ++k) atomicAdd(&kw.counters[20 + k], static_cast<unsigned long long>(pf_acc[k]));
+#endif
 #ifdef FR_DIAG
   if (lane == 0 && gw < 65536) g_fr_wave_times[2 * gw + 1] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
@@ -1030,6 +1061,14 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
   if (st) {
     unsigned long long cnt[32] = {};
     HIPCHK(hipMemcpy(cnt, c->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
+#ifdef FR_PROF
+    {
+      double tot = 0;
+      for (int k = 0; k < PF_N; ++k) tot += static_cast<double>(cnt[20 + k]);
+      fprintf(stderr, "FR_PROF {\"claim\": %.4f, \"reject\": %.4f, \"hit\": %.4f, \"shade\": %.4f, \"end\": %.4f, "
+              "\"wave_cycles\": %.4e}\n", cnt[20] / tot, cnt[21] / tot, cnt[22] / tot, cnt[23] / tot, cnt[24] / tot, tot);
+    }
+#endif
 #ifdef FR_DIAG
     unsigned long long dl[2], dr[2];
     HIPCHK(hipMemcpyFromSymbol(dl, HIP_SYMBOL(g_fr_diag_lens), sizeof(dl)));
