@@ -453,6 +453,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           const int r = plane_test(xyz(r4[0]), xyz(r4[1]), xyz(r4[2]), o, d, 0.001f, closest, t);
           if (r) t_last = t;
           h = r == 2;
+        } else if (k == FR_TRIANGLE) {
+          h = tri_root(xyz(r4[0]), xyz(r4[1]), xyz(r4[2]), o, d, 0.001f, closest, t);
         } else if (k == FR_OBB) {
           const float4 a = r4[0], b = r4[1], c = r4[2], e = r4[3];
           const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
@@ -487,6 +489,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
             n = divs(sub(pw, xyz(b0)), b0.w);
           } else if (kb == FR_PLANE) {
             n = scl(-1.0f, xyz(b1));
+          } else if (kb == FR_TRIANGLE) {
+            // precomputed winding normal, turned to face the ray except for dielectric
+            n = xyz(rb[3]);
+            if (sc.cls[best] != SC_DIELECTRIC && dot(n, d) > 0.0f) n = scl(-1.0f, n);
           } else {
             const float4 b2 = rb[2], b3 = rb[3];
             const ObbFrame f = obb_frame(xyz(b0), xyz(b1), xyz(b2), xyz(b3), o, d);
@@ -737,6 +743,18 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
         g[2] = make_float4(p.g[6], p.g[7], p.g[8], p.g[14]);
         g[3] = make_float4(p.g[9], p.g[10], p.g[11], 0.0f);
         break;
+      case FR_TRIANGLE: {
+        // v0, edges e1 = v1 - v0 and e2 = v2 - v0, and the unit winding normal
+        // unit(cross(e1, e2)), all in host f32 exactly as the oracle forms them
+        const V3 v0{p.g[0], p.g[1], p.g[2]};
+        const V3 e1 = sub(V3{p.g[3], p.g[4], p.g[5]}, v0), e2 = sub(V3{p.g[6], p.g[7], p.g[8]}, v0);
+        const V3 nw = unit(cross(e1, e2));
+        g[0] = make_float4(v0.x, v0.y, v0.z, 0.0f);
+        g[1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
+        g[2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
+        g[3] = make_float4(nw.x, nw.y, nw.z, 0.0f);
+        break;
+      }
       default: kind = FR_STUB;
     }
     const uint32_t cls = scatter_class(p);
@@ -766,7 +784,7 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   c->kinds = 0;
   for (const fr_prim& p : s->prims) {
     c->has_plane |= p.kind == FR_PLANE;
-    c->kinds |= 1u << (p.kind <= FR_STUB ? p.kind : FR_STUB);
+    c->kinds |= 1u << (p.kind <= FR_TRIANGLE ? p.kind : FR_STUB);
   }
   c->version = s->version;
   *out = c;

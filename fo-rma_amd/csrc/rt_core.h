@@ -295,6 +295,20 @@ FR_HD V3 slab_normal(const Slab& s, float t, V3 dd) {
   return axis_normal(k, comp(dd, k) > 0.0f ? 1.0f : -1.0f);
 }
 
+// Build-defined triangle: Moller-Trumbore in f32 with this order;
+// e1 = v1 - v0, e2 = v2 - v0 come precomputed (same host f32 ops as the oracle's).
+// NaN or infinite barycentrics (det = 0) fail the comparisons.
+FR_HD bool tri_root(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t_min, float t_max, float& t) {
+  const V3 pv = cross(d, e2);
+  const float inv_det = 1.0f / dot(e1, pv);
+  const V3 s = sub(o, v0);
+  const float u = dot(s, pv) * inv_det;
+  const V3 qv = cross(s, e1);
+  const float v = dot(d, qv) * inv_det;
+  t = dot(e2, qv) * inv_det;
+  return (u >= 0.0f) & (v >= 0.0f) & (u + v <= 1.0f) & (t > t_min) & (t < t_max);
+}
+
 // Oriented box: the same slab test in the box frame (rows ax, ay, az of world->local).
 struct ObbFrame {
   V3 dl, inv, ol;

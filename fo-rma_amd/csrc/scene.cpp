@@ -248,7 +248,108 @@ int material_of(const json::Value& obj, uint32_t& mat, V3& color, float& fuzz, i
   return FR_OK;
 }
 
-int map_object(const json::Value& obj, int index, fr_prim& out) {
+// ---- meshes as triangle lists (primitives/*.rs vertex and index tables) ----------
+
+struct Mesh {
+  std::vector<V3> v;        // local vertex positions
+  std::vector<uint32_t> i;  // triangles, three indices each
+};
+
+// f32 sector angle as the mesh generators write it: `i as f32 * 2.0 * PI / n as f32`
+// (circle.rs:67, cylinder.rs:76), and its cosine / sine rounded from double
+float sector_angle(uint32_t i, uint32_t n) {
+  const float kPiF = 3.14159265358979323846f;  // std::f32::consts::PI
+  return ((static_cast<float>(i) * 2.0f) * kPiF) / static_cast<float>(n);
+}
+float cos_rn(float a) { return static_cast<float>(cos(static_cast<double>(a))); }
+float sin_rn(float a) { return static_cast<float>(sin(static_cast<double>(a))); }
+
+Mesh mesh_triangle() {  // triangle.rs:6-13
+  return Mesh{{V3{0.0f, 0.5f, 0.0f}, V3{-0.5f, -0.5f, 0.0f}, V3{0.5f, -0.5f, 0.0f}}, {0, 1, 2}};
+}
+
+Mesh mesh_quad() {  // quad.rs:7-17
+  return Mesh{{V3{-0.5f, -0.5f, 0.0f}, V3{0.5f, -0.5f, 0.0f}, V3{0.5f, 0.5f, 0.0f}, V3{-0.5f, 0.5f, 0.0f}},
+              {0, 1, 2, 2, 3, 0}};
+}
+
+Mesh mesh_tetrahedron() {  // tetrahedron.rs:13-32 (X = 1)
+  const float X = 1.0f;
+  return Mesh{{V3{X, X, -X}, V3{X, -X, X}, V3{-X, X, X}, V3{-X, X, X}, V3{-X, -X, -X}, V3{X, X, -X},
+               V3{-X, X, X}, V3{X, -X, X}, V3{-X, -X, -X}, V3{X, X, -X}, V3{-X, -X, -X}, V3{X, -X, X}},
+              {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11}};
+}
+
+Mesh mesh_circle() {  // circle.rs:64-107: 36 sectors, radius 0.5, z = 0, centre last
+  const uint32_t n = 36;
+  Mesh m;
+  for (uint32_t k = 0; k < n; ++k) {
+    const float a = sector_angle(k, n);
+    m.v.push_back(V3{0.5f * cos_rn(a), 0.5f * sin_rn(a), 0.0f});
+  }
+  m.v.push_back(V3{0.0f, 0.0f, 0.0f});
+  for (uint32_t k = 0; k < n; ++k) {
+    m.i.push_back(k);
+    m.i.push_back((k + 1) % n);
+    m.i.push_back(n);
+  }
+  return m;
+}
+
+Mesh mesh_cylinder(uint32_t n) {  // cylinder.rs:72-174 with sector_count 30 (basics/scene.rs:90)
+  Mesh m;
+  const float ys[2] = {0.5f, -0.5f};
+  for (int cap = 0; cap < 2; ++cap) {  // top ring + centre, bottom ring + centre
+    for (uint32_t k = 0; k < n; ++k) {
+      const float a = sector_angle(k, n);
+      m.v.push_back(V3{0.5f * cos_rn(a), ys[cap], 0.5f * sin_rn(a)});
+    }
+    m.v.push_back(V3{0.0f, ys[cap], 0.0f});
+  }
+  for (int ring = 0; ring < 2; ++ring)  // side rings (same positions, own normals upstream)
+    for (uint32_t k = 0; k < n; ++k) {
+      const float a = sector_angle(k, n);
+      m.v.push_back(V3{0.5f * cos_rn(a), ys[ring], 0.5f * sin_rn(a)});
+    }
+  for (uint32_t k = 0; k < n; ++k) {  // top
+    m.i.insert(m.i.end(), {k, (k + 1) % n, n});
+  }
+  const uint32_t off = n + 1;
+  for (uint32_t k = 0; k < n; ++k) {  // bottom
+    m.i.insert(m.i.end(), {(k + 1) % n + off, k + off, n + off});
+  }
+  const uint32_t side = 2 * (n + 1);
+  for (uint32_t k = 0; k < n; ++k) {  // sides, two triangles per sector
+    m.i.insert(m.i.end(), {(k + 1) % n + side, k + side, (k + 1) % n + side + n});
+    m.i.insert(m.i.end(), {k + side + n, (k + 1) % n + side + n, k + side});
+  }
+  return m;
+}
+
+// Model transform of one vertex, f32, in this order:
+// w = ((ax.x (s.x l.x) + ax.y (s.y l.y)) + ax.z (s.z l.z)) + pos, per component
+V3 to_world(const Axes& ax, V3 s, V3 pos, V3 l) {
+  const float sx = s.x * l.x, sy = s.y * l.y, sz = s.z * l.z;
+  return V3{((ax.x.x * sx + ax.y.x * sy) + ax.z.x * sz) + pos.x, ((ax.x.y * sx + ax.y.y * sy) + ax.z.y * sz) + pos.y,
+            ((ax.x.z * sx + ax.y.z * sy) + ax.z.z * sz) + pos.z};
+}
+
+void append_mesh(const Mesh& m, const Axes& ax, V3 scale, V3 pos, const fr_prim& base, std::vector<fr_prim>& out) {
+  std::vector<V3> w(m.v.size());
+  for (size_t k = 0; k < m.v.size(); ++k) w[k] = to_world(ax, scale, pos, m.v[k]);
+  for (size_t t = 0; t + 2 < m.i.size(); t += 3) {
+    fr_prim p = base;
+    p.kind = FR_TRIANGLE;
+    to_arr(w[m.i[t]], p.g);
+    to_arr(w[m.i[t + 1]], p.g + 3);
+    to_arr(w[m.i[t + 2]], p.g + 6);
+    out.push_back(p);
+  }
+}
+
+// One JSON object -> its tracer primitives, appended to `list` (one for sphere / cube /
+// axis-aligned quad, a triangle list for the other meshes).
+int map_object(const json::Value& obj, int index, std::vector<fr_prim>& list) {
   if (obj.type != json::Value::Object) return set_error(FR_EPARSE, "objects[%d] is not an object", index);
   const json::Value* mesh = obj.get("mesh");
   if (!mesh || mesh->type != json::Value::String)
@@ -264,6 +365,7 @@ int map_object(const json::Value& obj, int index, fr_prim& out) {
   int rc = material_of(obj, mat, color, fuzz, index);
   if (rc) return rc;
 
+  fr_prim out;
   memset(&out, 0, sizeof(out));
   out.material = mat;
   to_arr(color, out.color);
@@ -275,6 +377,7 @@ int map_object(const json::Value& obj, int index, fr_prim& out) {
     out.kind = FR_SPHERE;
     to_arr(pos, out.g);
     out.g[3] = 0.5f * scale.x;
+    list.push_back(out);
     return FR_OK;
   }
   if (m == "cube") {
@@ -302,33 +405,50 @@ int map_object(const json::Value& obj, int index, fr_prim& out) {
       out.g[13] = h[1];
       out.g[14] = h[2];
     }
+    list.push_back(out);
     return FR_OK;
   }
-  if (m == "quad") {
-    // primitives/quad.rs:7-12: unit quad in local z = 0 with normal -z. The reference
-    // Plane's orientation is -normal = R*(0,0,1); its extent is per world axis.
-    int perm[3];
-    float sign[3];
-    if (!signed_permutation(ax, perm, sign))
-      return set_error(FR_EPARSE, "objects[%d]: quad rotation is not axis-aligned (Plane bounds are per world axis)",
-                       index);
-    const float hl[3] = {0.5f * scale.x, 0.5f * scale.y, 0.0f};
-    float size[3], orient[3] = {0.0f, 0.0f, 0.0f};
-    for (int j = 0; j < 3; ++j) size[perm[j]] = hl[j];
-    size[perm[2]] = size[perm[2]] + 1e-3f;
-    orient[perm[2]] = sign[2];
-    out.kind = FR_PLANE;
-    to_arr(pos, out.g);
-    out.g[3] = orient[0];
-    out.g[4] = orient[1];
-    out.g[5] = orient[2];
-    out.g[6] = size[0];
-    out.g[7] = size[1];
-    out.g[8] = size[2];
+  if (m == "triangle") {
+    append_mesh(mesh_triangle(), ax, scale, pos, out, list);
     return FR_OK;
   }
-  return set_error(FR_EPARSE, "objects[%d]: mesh '%s' has no tracer primitive yet (SURVEY §8f row 1)", index,
-                   m.c_str());
+  if (m == "circle") {
+    append_mesh(mesh_circle(), ax, scale, pos, out, list);
+    return FR_OK;
+  }
+  if (m == "cylinder") {
+    append_mesh(mesh_cylinder(30), ax, scale, pos, out, list);
+    return FR_OK;
+  }
+  if (m == "tetrahedron") {
+    append_mesh(mesh_tetrahedron(), ax, scale, pos, out, list);
+    return FR_OK;
+  }
+  // "quad" and any other mesh name (basics/scene.rs:93-95 falls back to Quad)
+  // primitives/quad.rs:7-12: unit quad in local z = 0 with normal -z. Axis-aligned quads
+  // become the reference Plane (orientation = -normal = R*(0,0,1), extent per world
+  // axis); any other rotation becomes the quad's two triangles.
+  int perm[3];
+  float sign[3];
+  if (!signed_permutation(ax, perm, sign)) {
+    append_mesh(mesh_quad(), ax, scale, pos, out, list);
+    return FR_OK;
+  }
+  const float hl[3] = {0.5f * scale.x, 0.5f * scale.y, 0.0f};
+  float size[3], orient[3] = {0.0f, 0.0f, 0.0f};
+  for (int j = 0; j < 3; ++j) size[perm[j]] = hl[j];
+  size[perm[2]] = size[perm[2]] + 1e-3f;
+  orient[perm[2]] = sign[2];
+  out.kind = FR_PLANE;
+  to_arr(pos, out.g);
+  out.g[3] = orient[0];
+  out.g[4] = orient[1];
+  out.g[5] = orient[2];
+  out.g[6] = size[0];
+  out.g[7] = size[1];
+  out.g[8] = size[2];
+  list.push_back(out);
+  return FR_OK;
 }
 
 }  // namespace
@@ -400,7 +520,7 @@ int fr_update_delta(uint8_t keys, float dt, float out[3]) {
 int fr_scene_create(const fr_prim* prims, uint32_t n, fr_scene** out) {
   if (!out || (n && !prims)) return set_error(FR_EARG, "fr_scene_create: bad arguments");
   for (uint32_t i = 0; i < n; ++i)
-    if (prims[i].kind > FR_STUB) return set_error(FR_EARG, "fr_scene_create: prims[%u] has unknown kind %u", i, prims[i].kind);
+    if (prims[i].kind > FR_TRIANGLE) return set_error(FR_EARG, "fr_scene_create: prims[%u] has unknown kind %u", i, prims[i].kind);
   fr_scene* s = new (std::nothrow) fr_scene();
   if (!s) return set_error(FR_ENOMEM, "fr_scene_create: out of memory");
   s->prims.assign(prims, prims + n);
@@ -448,9 +568,10 @@ int fr_scene_from_json(const char* text, size_t len, uint32_t width, uint32_t he
   float cq[4], fov;
   if (!vec3_of(cam->get("position"), cpos) || !quat_of(cam->get("rotation"), cq) || !num_f32(cam->get("fov"), fov))
     return set_error(FR_EPARSE, "camera needs position{x,y,z}, rotation{x,y,z,w}, fov");
-  std::vector<fr_prim> prims(objects->items.size());
+  std::vector<fr_prim> prims;
+  prims.reserve(objects->items.size());
   for (size_t i = 0; i < objects->items.size(); ++i) {
-    int rc = map_object(objects->items[i], static_cast<int>(i), prims[i]);
+    int rc = map_object(objects->items[i], static_cast<int>(i), prims);
     if (rc) return rc;
   }
   if (cam_out) {

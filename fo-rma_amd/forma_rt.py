@@ -28,7 +28,7 @@ LIB_PATH = os.environ.get("FORMA_RT_LIB") or os.path.join(HERE, "libforma_rt.so"
 SCENES_DIR = os.path.join(HERE, "scenes")
 
 FR_OK, FR_EARG, FR_EPARSE, FR_EHIP, FR_ENODEV, FR_ENOMEM = 0, -1, -2, -3, -4, -5
-FR_SPHERE, FR_PLANE, FR_AABB, FR_OBB, FR_STUB = 0, 1, 2, 3, 4
+FR_SPHERE, FR_PLANE, FR_AABB, FR_OBB, FR_STUB, FR_TRIANGLE = 0, 1, 2, 3, 4, 5
 FR_LAMBERTIAN, FR_METAL, FR_DIELECTRIC, FR_LIGHT = 0, 1, 2, 3
 FR_FLAG_WRITE_U8 = 1
 MAX_DEPTH = 50  # tracer.rs:10
@@ -226,6 +226,18 @@ class Box(Hitable):
 
     def geometry(self):
         return tuple(self.mn) + tuple(self.mx)
+
+
+class Triangle(Hitable):
+    """The build's triangle (FR_TRIANGLE), vertices v0, v1, v2 in winding order."""
+    kind = FR_TRIANGLE
+
+    def __init__(self, v0, v1, v2, material, color, fuzz):
+        super().__init__(material, color, fuzz)
+        self.v = (tuple(v0), tuple(v1), tuple(v2))
+
+    def geometry(self):
+        return self.v[0] + self.v[1] + self.v[2]
 
 
 class Stub(Hitable):

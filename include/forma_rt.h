@@ -61,6 +61,7 @@ extern "C" {
 #define FR_AABB 2u   /* build-defined axis-aligned box (JSON "cube" with a signed-permutation rotation) */
 #define FR_OBB 3u    /* build-defined oriented box (JSON "cube", any other rotation) */
 #define FR_STUB 4u   /* shapes/aabb.rs / rectangle.rs: hit() and scatter() always false */
+#define FR_TRIANGLE 5u /* build-defined triangle: JSON triangle/circle/cylinder/tetrahedron meshes, tilted quads */
 
 /* material ids as the reference stores them (u8 `material` field) */
 #define FR_LAMBERTIAN 0u /* sphere.rs:84-89, plane.rs:101-106 */
@@ -80,6 +81,7 @@ extern "C" {
  *   FR_OBB    : g[0..2] center, g[3..5] local x axis, g[6..8] local y axis, g[9..11] local z axis
  *               (unit rows of the world->local rotation), g[12..14] half extents
  *   FR_STUB   : unused
+ *   FR_TRIANGLE: g[0..2], g[3..5], g[6..8] the world vertices v0, v1, v2 (winding v0 -> v1 -> v2)
  * `material` is the raw reference id; unknown ids fall back as sphere.rs:68 / plane.rs:55 do.
  */
 typedef struct fr_prim {

@@ -393,6 +393,32 @@ struct Obb : BoxBase {
   }
 };
 
+// Build-defined triangle: Moller-Trumbore, f32, fixed order; the
+// JSON triangle/circle/cylinder/tetrahedron meshes and tilted quads become lists of
+// these. Normal: unit(cross(e1, e2)) by winding; for every material but dielectric it
+// is turned to face the incoming ray (the raster meshes are double-faced).
+struct Triangle : BoxBase {
+  Vec3 v0, v1, v2;
+  bool hit(Ray ray, float t_min, float t_max, HitRecord& rec) const override {
+    const Vec3 e1 = v1 - v0, e2 = v2 - v0;
+    const Vec3 d = ray.direction();
+    const Vec3 pv = Vec3::cross(d, e2);
+    const float inv_det = 1.0f / Vec3::dot(e1, pv);
+    const Vec3 s = ray.origin() - v0;
+    const float u = Vec3::dot(s, pv) * inv_det;
+    const Vec3 qv = Vec3::cross(s, e1);
+    const float v = Vec3::dot(d, qv) * inv_det;
+    const float t = Vec3::dot(e2, qv) * inv_det;
+    if (!(u >= 0.0f && v >= 0.0f && u + v <= 1.0f && t > t_min && t < t_max)) return false;
+    rec.t = t;
+    rec.p = ray.point_at(t);
+    Vec3 n = Vec3::cross(e1, e2).unit_vector();
+    if (material != 2u && Vec3::dot(n, d) > 0.0f) n = -1.0f * n;
+    rec.normal = n;
+    return true;
+  }
+};
+
 // ---- cpu_ray_tracer/camera.rs -------------------------------------------------
 const float PI = 3.14159265359f;  // :5
 
@@ -557,6 +583,17 @@ std::vector<std::unique_ptr<Hitable>> build(const or_prim* prims, uint32_t n) {
         s->ax[1] = Vec3(p.g[6], p.g[7], p.g[8]);
         s->ax[2] = Vec3(p.g[9], p.g[10], p.g[11]);
         s->half = Vec3(p.g[12], p.g[13], p.g[14]);
+        s->material = p.material;
+        s->color = color;
+        s->fuzz = p.fuzz;
+        out.push_back(std::move(s));
+        break;
+      }
+      case 5: {
+        auto s = std::make_unique<Triangle>();
+        s->v0 = Vec3(p.g[0], p.g[1], p.g[2]);
+        s->v1 = Vec3(p.g[3], p.g[4], p.g[5]);
+        s->v2 = Vec3(p.g[6], p.g[7], p.g[8]);
         s->material = p.material;
         s->color = color;
         s->fuzz = p.fuzz;

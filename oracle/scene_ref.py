@@ -14,12 +14,13 @@ by the product.
 from __future__ import annotations
 
 import json
+import math
 
 import numpy as np
 
 F = np.float32
 
-SPHERE, PLANE, AABB, OBB, STUB = 0, 1, 2, 3, 4
+SPHERE, PLANE, AABB, OBB, STUB, TRIANGLE = 0, 1, 2, 3, 4, 5
 LAMBERTIAN, METAL, DIELECTRIC, LIGHT = 0, 1, 2, 3
 
 # color_utils.rs:101-109 (CP0)
@@ -145,7 +146,84 @@ class MappingError(ValueError):
     pass
 
 
+# ---- meshes as triangle lists (primitives/*.rs vertex/index tables) ----
+
+def _angle(i, n):
+    """`i as f32 * 2.0 * PI / n as f32` (circle.rs:67, cylinder.rs:76) in f32."""
+    return ((F(i) * F(2.0)) * F(3.14159265358979323846)) / F(n)
+
+
+def _cos(a):
+    return F(math.cos(float(a)))
+
+
+def _sin(a):
+    return F(math.sin(float(a)))
+
+
+def mesh_triangle():  # triangle.rs:6-13
+    return [(0.0, 0.5, 0.0), (-0.5, -0.5, 0.0), (0.5, -0.5, 0.0)], [0, 1, 2]
+
+
+def mesh_quad():  # quad.rs:7-17
+    return [(-0.5, -0.5, 0.0), (0.5, -0.5, 0.0), (0.5, 0.5, 0.0), (-0.5, 0.5, 0.0)], [0, 1, 2, 2, 3, 0]
+
+
+def mesh_tetrahedron():  # tetrahedron.rs:13-32
+    X = 1.0
+    v = [(X, X, -X), (X, -X, X), (-X, X, X), (-X, X, X), (-X, -X, -X), (X, X, -X),
+         (-X, X, X), (X, -X, X), (-X, -X, -X), (X, X, -X), (-X, -X, -X), (X, -X, X)]
+    return v, list(range(12))
+
+
+def mesh_circle(n=36):  # circle.rs:64-107
+    v = [(F(0.5) * _cos(_angle(k, n)), F(0.5) * _sin(_angle(k, n)), 0.0) for k in range(n)] + [(0.0, 0.0, 0.0)]
+    idx = []
+    for k in range(n):
+        idx += [k, (k + 1) % n, n]
+    return v, idx
+
+
+def mesh_cylinder(n=30):  # cylinder.rs:72-174, sector_count 30 (basics/scene.rs:90)
+    v = []
+    for y in (0.5, -0.5):
+        v += [(F(0.5) * _cos(_angle(k, n)), y, F(0.5) * _sin(_angle(k, n))) for k in range(n)]
+        v.append((0.0, y, 0.0))
+    for y in (0.5, -0.5):
+        v += [(F(0.5) * _cos(_angle(k, n)), y, F(0.5) * _sin(_angle(k, n))) for k in range(n)]
+    idx = []
+    for k in range(n):
+        idx += [k, (k + 1) % n, n]
+    off = n + 1
+    for k in range(n):
+        idx += [(k + 1) % n + off, k + off, n + off]
+    side = 2 * (n + 1)
+    for k in range(n):
+        idx += [(k + 1) % n + side, k + side, (k + 1) % n + side + n]
+        idx += [k + side + n, (k + 1) % n + side + n, k + side]
+    return v, idx
+
+
+def to_world(axes, scale, pos, l):
+    """w = ((ax.x (s.x l.x) + ax.y (s.y l.y)) + ax.z (s.z l.z)) + pos, f32 per component."""
+    sx, sy, sz = scale[0] * F(l[0]), scale[1] * F(l[1]), scale[2] * F(l[2])
+    ax, ay, az = axes
+    return [((ax[i] * sx + ay[i] * sy) + az[i] * sz) + pos[i] for i in range(3)]
+
+
+def mesh_prims(mesh, axes, scale, pos, material, color, fuzz):
+    verts, idx = mesh
+    w = [to_world(axes, scale, pos, v) for v in verts]
+    return [prim(TRIANGLE, material, color, fuzz, w[idx[t]] + w[idx[t + 1]] + w[idx[t + 2]])
+            for t in range(0, len(idx) - 2, 3)]
+
+
+MESHES = {"triangle": mesh_triangle, "circle": mesh_circle, "cylinder": mesh_cylinder,
+          "tetrahedron": mesh_tetrahedron}
+
+
 def map_object(o):
+    """One JSON object -> its list of tracer primitives."""
     mesh, mat_name = o["mesh"], o["material"]
     pos, q, scale = _v3(o["position"]), _q(o["rotation"]), _v3(o["scale"])
     if mat_name == "DiffuseTexture":
@@ -163,7 +241,7 @@ def map_object(o):
     axes = quat_axes(*q)
     half = F(0.5)
     if mesh == "sphere":
-        return prim(SPHERE, material, color, fuzz, pos + [half * scale[0]])
+        return [prim(SPHERE, material, color, fuzz, pos + [half * scale[0]])]
     if mesh == "cube":
         h = [half * s for s in scale]
         perm = signed_permutation(axes)
@@ -173,22 +251,23 @@ def map_object(o):
                 hw[i] = h[j]
             mn = [pos[i] - hw[i] for i in range(3)]
             mx = [pos[i] + hw[i] for i in range(3)]
-            return prim(AABB, material, color, fuzz, mn + mx)
+            return [prim(AABB, material, color, fuzz, mn + mx)]
         g = pos + list(axes[0]) + list(axes[1]) + list(axes[2]) + h
-        return prim(OBB, material, color, fuzz, g)
-    if mesh == "quad":
-        perm = signed_permutation(axes)
-        if perm is None:
-            raise MappingError("quad rotation is not axis-aligned")
-        hl = [half * scale[0], half * scale[1], F(0.0)]
-        size, orient = [F(0.0)] * 3, [F(0.0)] * 3
-        for j, (i, _) in enumerate(perm):
-            size[i] = hl[j]
-        iz, sz = perm[2]
-        size[iz] = size[iz] + F(1e-3)
-        orient[iz] = F(sz)
-        return prim(PLANE, material, color, fuzz, pos + orient + size)
-    raise MappingError(f"mesh {mesh!r} has no tracer primitive")
+        return [prim(OBB, material, color, fuzz, g)]
+    if mesh in MESHES:
+        return mesh_prims(MESHES[mesh](), axes, scale, pos, material, color, fuzz)
+    # "quad" and any unknown mesh (basics/scene.rs:93-95 falls back to Quad)
+    perm = signed_permutation(axes)
+    if perm is None:
+        return mesh_prims(mesh_quad(), axes, scale, pos, material, color, fuzz)
+    hl = [half * scale[0], half * scale[1], F(0.0)]
+    size, orient = [F(0.0)] * 3, [F(0.0)] * 3
+    for j, (i, _) in enumerate(perm):
+        size[i] = hl[j]
+    iz, sz = perm[2]
+    size[iz] = size[iz] + F(1e-3)
+    orient[iz] = F(sz)
+    return [prim(PLANE, material, color, fuzz, pos + orient + size)]
 
 
 def camera_of(scene_json):
@@ -206,4 +285,4 @@ def load_json(text):
     for key in ("camera", "lights", "objects"):
         if key not in d:
             raise MappingError(f"missing field {key!r}")
-    return [map_object(o) for o in d["objects"]], camera_of(d)
+    return [p for o in d["objects"] for p in map_object(o)], camera_of(d)

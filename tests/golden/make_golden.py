@@ -29,6 +29,9 @@ CASES = {
     "scene03_obb_32x32_s4_d4": ("json:scene_03", 32, 32, 4, 4, 0x5EED),
     "scene08_64x36_s4_d8": ("json:scene_08", 64, 36, 4, 8, 0x5EED),
     "scene08_33x17_s3_d8_seed7": ("json:scene_08", 33, 17, 3, 8, 7),
+    "scene02_mesh_48x27_s3_d8": ("json:scene_02", 48, 27, 3, 8, 0x5EED),
+    "scene06_cyl_48x27_s2_d8": ("json:scene_06", 48, 27, 2, 8, 0x5EED),
+    "scene09_tet_40x40_s4_d8": ("json:scene_09", 40, 40, 4, 8, 0x5EED),
 }
 
 
@@ -49,7 +52,9 @@ def render_case(name):
 
 
 def main():
-    for name in CASES:
+    import sys
+    names = sys.argv[1:] or list(CASES)  # regenerate only the named cases if given
+    for name in names:
         mean, u8, cnt = render_case(name)
         np.savez_compressed(os.path.join(OUT, f"{name}.npz"), mean=mean, u8=u8,
                             counters=np.array([cnt["segments"], cnt["hits"], cnt["samples"], cnt["scatters"]],

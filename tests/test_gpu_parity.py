@@ -201,7 +201,7 @@ def random_scene(seed, n=12):
     r = np.random.default_rng(seed)
     prims = []
     for i in range(n):
-        kind = r.choice([S.SPHERE, S.SPHERE, S.PLANE, S.AABB, S.OBB, S.STUB])
+        kind = r.choice([S.SPHERE, S.SPHERE, S.PLANE, S.AABB, S.OBB, S.STUB, S.TRIANGLE, S.TRIANGLE])
         mat = int(r.integers(0, 5))
         col = r.uniform(0.1, 1.0, 3)
         fuzz = float(r.uniform(0, 1))
@@ -223,6 +223,9 @@ def random_scene(seed, n=12):
             ax = S.quat_axes(*q)
             prims.append(S.prim(S.OBB, mat, col, fuzz, list(c) + list(ax[0]) + list(ax[1]) + list(ax[2])
                                 + list(r.uniform(0.1, 1.0, 3))))
+        elif kind == S.TRIANGLE:
+            v = [list(c + r.uniform(-1.2, 1.2, 3)) for _ in range(3)]
+            prims.append(S.prim(S.TRIANGLE, mat, col, fuzz, v[0] + v[1] + v[2]))
         else:
             prims.append(S.prim(S.STUB, mat, col, fuzz))
     prims.append(S.sphere((0.0, -100.5, -1.0), 100.0, 0, (0.5, 0.5, 0.5), 0.0))

@@ -147,6 +147,37 @@ def test_obb_matches_aabb_for_identity_axes():
     assert best == 0 and rec[0] == 4.0 and list(rec[4:]) == [0.0, 0.0, 1.0]
 
 
+def _tri(v0, v1, v2, material=0):
+    return S.prim(S.TRIANGLE, material, (1, 1, 1), 0.0, list(v0) + list(v1) + list(v2))
+
+
+def test_triangle_hit_barycentric_bounds_and_facing_normal():
+    # triangle in z = -4; counter-clockwise seen from +z, so the winding normal is +z
+    t = _tri((-1.0, -1.0, -4.0), (1.0, -1.0, -4.0), (0.0, 1.0, -4.0))
+    best, rec = O.closest_hit([t], (0, 0, 0), (0, 0, -1))
+    assert best == 0 and rec[0] == 4.0 and list(rec[1:4]) == [0.0, 0.0, -4.0] and list(rec[4:]) == [0, 0, 1.0]
+    # from behind: the normal still faces the ray (double-faced meshes)
+    best, rec = O.closest_hit([t], (0, 0, -8.0), (0, 0, 1))
+    assert best == 0 and rec[0] == 4.0 and list(rec[4:]) == [0, 0, -1.0]
+    # dielectric keeps the winding normal (inside/outside for refraction)
+    best, rec = O.closest_hit([_tri((-1.0, -1.0, -4.0), (1.0, -1.0, -4.0), (0.0, 1.0, -4.0), 2)], (0, 0, -8.0), (0, 0, 1))
+    assert best == 0 and list(rec[4:]) == [0, 0, 1.0]
+    # outside the edges, behind t_min, and parallel rays miss
+    assert O.closest_hit([t], (1.5, 0, 0), (0, 0, -1))[0] == -1
+    assert O.closest_hit([t], (0, 0, -4.0005), (0, 0, 1))[0] == -1      # t = 0.0005 < t_min 0.001
+    assert O.closest_hit([t], (0, 0, 0), (1, 0, 0))[0] == -1            # det = 0
+    # a vertex and an edge point are inside (u, v >= 0, u + v <= 1 are closed)
+    assert O.closest_hit([t], (-1.0, -1.0, 0), (0, 0, -1))[0] == 0
+    assert O.closest_hit([t], (0.0, -1.0, 0), (0, 0, -1))[0] == 0
+
+
+def test_triangle_list_order_and_ties():
+    a = _tri((-1.0, -1.0, -4.0), (1.0, -1.0, -4.0), (0.0, 1.0, -4.0))
+    b = _tri((-1.0, -1.0, -6.0), (1.0, -1.0, -6.0), (0.0, 1.0, -6.0))
+    assert O.closest_hit([b, a], (0, 0, 0), (0, 0, -1))[0] == 1
+    assert O.closest_hit([a, a], (0, 0, 0), (0, 0, -1))[0] == 0
+
+
 def test_camera_new_basis():
     # camera.rs:24-60 at 2:1 aspect: w = +z, u = +x, v = +y, tan(30deg) half height
     c = O.camera_to_array(O.camera_new(200, 100))

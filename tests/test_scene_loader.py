@@ -11,7 +11,8 @@ import pytest
 from oracle import oracle_py as O
 from oracle import scene_ref as S
 
-SCENES_OK = ["scene_01", "scene_03", "scene_04", "scene_05", "scene_07", "scene_08"]
+SCENES_OK = ["scene_01", "scene_02", "scene_03", "scene_04", "scene_05", "scene_06", "scene_07", "scene_08",
+             "scene_09"]
 REF_SCENES = "/root/reference/scenes"
 
 
@@ -66,11 +67,47 @@ def test_translate_rotate_only_move_planes(fr):
     _same(sc.prims(), S.BUILTIN[3]())
 
 
-@pytest.mark.parametrize("name,msg", [("scene_02", "circle"), ("scene_06", "cylinder"), ("scene_09", "tetrahedron")])
-def test_unsupported_meshes_are_parse_errors(fr, name, msg):
-    with pytest.raises(fr.ForMaError) as e:
-        fr.Scene.from_file(fr.scene_path(name), 8, 8)
-    assert e.value.code == fr.FR_EPARSE and msg in str(e.value)
+@pytest.mark.parametrize("name,kinds", [
+    ("scene_02", {1: 1, 5: 36 + 120}),        # quad (Plane) + circle (36) + cylinder (30 sectors: 120)
+    ("scene_06", {1: 1, 5: 12 * 120}),        # quad + 12 cylinders
+    ("scene_09", {5: 4})])                    # tetrahedron
+def test_meshes_become_triangle_lists(fr, name, kinds):
+    """basics/scene.rs:81-95 meshes: circle/cylinder/tetrahedron/triangle -> triangle lists
+    (primitives/*.rs vertex and index tables)."""
+    import collections
+    sc = fr.Scene.from_file(fr.scene_path(name), 64, 36)
+    assert dict(collections.Counter(p.kind for p in sc.prims())) == kinds
+
+
+def _one_object(mesh, rot=(0.0, 0.0, 0.0, 1.0), scale=(1.0, 1.0, 1.0)):
+    return json.dumps({"camera": {"position": {"x": 0, "y": 0, "z": -5}, "rotation": {"x": 0, "y": 0, "z": 0, "w": 1},
+                                  "fov": 60}, "lights": [],
+                       "objects": [{"mesh": mesh, "material": "DiffuseColorMaterial",
+                                    "position": {"x": 0.25, "y": -0.5, "z": 1.0},
+                                    "rotation": dict(zip("xyzw", rot)), "scale": dict(zip("xyz", scale))}]})
+
+
+@pytest.mark.parametrize("mesh,rot,n", [
+    ("triangle", (0.0, 0.0, 0.0, 1.0), 1),
+    ("triangle", (0.1913417, 0.0, 0.0, 0.98078528), 1),
+    ("tetrahedron", (0.46193978, 0.1913417, 0.1913417, 0.84462326), 4),
+    ("circle", (0.0, 0.70710677, 0.0, 0.70710677), 36),
+    ("cylinder", (0.3, 0.1, -0.2, 0.9273618), 120),
+    ("quad", (0.1913417, 0.0, 0.0, 0.98078528), 2),     # tilted quad: its two triangles
+    ("pyramid", (0.1913417, 0.0, 0.0, 0.98078528), 2),  # unknown mesh -> Quad (basics/scene.rs:93-95)
+    ("pyramid", (0.0, 0.0, 0.0, 1.0), 1)])              # ... axis-aligned: the Plane
+def test_mesh_vertices_match_oracle(fr, mesh, rot, n):
+    text = _one_object(mesh, rot, (2.0, 0.5, 3.0))
+    sc = fr.Scene.from_json(text, 16, 16)
+    prims = S.load_json(text)[0]
+    assert len(prims) == n
+    _same(sc.prims(), prims)
+
+
+def test_triangle_mesh_vertex_positions():
+    # triangle.rs:6-13 under identity rotation, scale (2, 0.5, 3), position (0.25, -0.5, 1)
+    p = S.load_json(_one_object("triangle", scale=(2.0, 0.5, 3.0)))[0][0]
+    assert list(p["g"][:9]) == [0.25, -0.25, 1.0, -0.75, -0.75, 1.0, 1.25, -0.75, 1.0]
 
 
 @pytest.mark.parametrize("text", [b"", b"{", b"[1,2]", b'{"camera": {}}', b'{"camera":{"position":{"x":0,"y":0,"z":0},'
