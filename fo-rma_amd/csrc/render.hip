@@ -20,6 +20,7 @@
 #include <chrono>
 #include <thread>
 
+#include "bvh.h"
 #include "internal.h"
 #ifdef FR_DIAG
 // rejection-loop trip counters (wave trips via first active lane, lane tries)
@@ -80,6 +81,8 @@ struct DeviceCopy {
   uint32_t kinds = 0;  // bit k set if a primitive of kind k is present
   size_t off_kind = 0, off_g0 = 0, off_g1 = 0, off_g2 = 0, off_g3 = 0, off_mat = 0, off_cls = 0, off_att = 0;
   size_t off_rec = 0;
+  size_t off_bvh = 0, off_bvh_order = 0;
+  uint32_t bvh_n = 0;  // BVH nodes (0 = in-order loop only)
 };
 
 struct KScene {
@@ -94,7 +97,10 @@ struct KScene {
   const float4* __restrict__ mat;   // colour rgb, fuzz
   const uint32_t* __restrict__ cls; // effective ScatterClass
   const float4* __restrict__ att;   // attenuation rgb (colour, or 1 for light)
+  const float4* __restrict__ bvh;   // BVH nodes, two float4 each (bvh.h), or null
+  const uint32_t* __restrict__ bvh_order;  // primitive index of each leaf slot
   uint32_t n;
+  uint32_t bvh_n;                   // node count (0: no BVH)
 };
 
 struct KParams {
@@ -264,7 +270,7 @@ enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 // amdgpu_num_sgpr caps the scalar registers (MI355X_MICROARCH.md "Residency and
 // cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
 // admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
-template <int KS, bool HAS_PLANE, int KREJ, int MAXD>
+template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) void trace_kernel(
     KScene sc, KCam cam, KParams kp, KWork kw) {
   // LDS: [attenuation rgb, n_att entries][stack: MAXD ? MAXD x kBlock u16 : max_depth x kBlock u32]
@@ -435,7 +441,52 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       const float a_dd = dot(d, d);
       float closest = FLT_MAX, t_last = 0.0f;
       int best = -1;
-      for (uint32_t ii = 0; ii < sc.n; ++ii) {
+      if (BVH) {
+        // Threaded BVH walk (bvh.h), one node index per lane. A primitive's candidate t
+        // does not depend on t_max, so the list loop's winner is the least (t, index):
+        // a primitive listed before the current winner may also take an exact tie,
+        // tested with t_max one ulp above closest. Boxes are padded, so no primitive
+        // the list loop accepts is culled.
+        uint32_t ni = 0;
+        while (ni < sc.bvh_n) {
+          const float4 na = sc.bvh[2 * ni], nb = sc.bvh[2 * ni + 1];
+          const Slab sl = slab3(xyz(na), xyz(nb), o, inv);
+          const bool enter = (sl.tn <= sl.tf) & (sl.tf >= 0.001f) & (sl.tn <= closest);
+          const uint32_t leaf = __float_as_uint(nb.w);
+          if (enter && leaf) {
+            const uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
+            for (uint32_t kk = 0; kk < cnt; ++kk) {
+              const uint32_t i = sc.bvh_order[first + kk];
+              const float4* r = sc.rec + 4 * i;
+              const float tmax =
+                  static_cast<int>(i) < best ? __uint_as_float(__float_as_uint(closest) + 1u) : closest;
+              const uint32_t k = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(r[3].w);
+              float t = 0.0f;
+              bool h = false;
+              if (k == FR_SPHERE) {
+                const float4 g = r[0];
+                h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, tmax, t);
+              } else if (k == FR_AABB) {
+                h = slab_root(slab3(xyz(r[0]), xyz(r[1]), o, inv), 0.001f, tmax, t);
+              } else if (k == FR_TRIANGLE) {
+                h = tri_root(xyz(r[0]), xyz(r[1]), xyz(r[2]), o, d, 0.001f, tmax, t);
+              } else if (k == FR_OBB) {
+                const float4 a = r[0], b = r[1], c = r[2], e = r[3];
+                const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
+                h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, tmax, t);
+              }
+              if (h) {
+                closest = t;
+                best = static_cast<int>(i);
+              }
+            }
+            ni = __float_as_uint(na.w);
+          } else {
+            ni = enter ? ni + 1u : __float_as_uint(na.w);
+          }
+        }
+      }
+      for (uint32_t ii = 0; ii < (BVH ? 0u : sc.n); ++ii) {
         // the index is wave-uniform; say so, or the compiler may fall back to vector loads
         const uint32_t i = __builtin_amdgcn_readfirstlane(ii);
         const RecRef r4 = rec_at(sc.rec, i);  // scalar loads
@@ -702,6 +753,12 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   }
   const uint32_t n = static_cast<uint32_t>(s->prims.size());
   const size_t m = n ? n : 1;  // never hand the kernel a null array
+  // BVH for plane-free scenes of kBvhMinPrims or more (bvh.h)
+  bool any_plane = false;
+  for (const fr_prim& p : s->prims) any_plane |= p.kind == FR_PLANE;
+  std::vector<BvhNode> bvh_nodes;
+  std::vector<uint32_t> bvh_order;
+  if (!any_plane && n >= kBvhMinPrims) build_bvh(s->prims, bvh_nodes, bvh_order);
   size_t off = 0;
   c->off_kind = off;
   off = align_up(off + m * 4, 256);
@@ -721,7 +778,16 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   off = align_up(off + m * 16, 256);
   c->off_rec = off;
   off = align_up(off + m * 64, 256);
+  c->off_bvh = off;
+  off = align_up(off + (bvh_nodes.size() ? bvh_nodes.size() : 1) * sizeof(BvhNode), 256);
+  c->off_bvh_order = off;
+  off = align_up(off + (bvh_order.size() ? bvh_order.size() : 1) * 4, 256);
   std::vector<unsigned char> host(off, 0);
+  if (!bvh_nodes.empty()) {
+    memcpy(&host[c->off_bvh], bvh_nodes.data(), bvh_nodes.size() * sizeof(BvhNode));
+    memcpy(&host[c->off_bvh_order], bvh_order.data(), bvh_order.size() * 4);
+  }
+  c->bvh_n = static_cast<uint32_t>(bvh_nodes.size());
   for (uint32_t i = 0; i < n; ++i) {
     const fr_prim& p = s->prims[i];
     uint32_t kind = p.kind;
@@ -834,25 +900,36 @@ struct fr_ctx {
 // Picks the specialisation: single-kind scenes (all boxes, all spheres) drop the
 // per-primitive kind switch; HAS_PLANE adds the stale-record bookkeeping; small depth
 // uses the u16 stack with the unrolled unwind.
-template <int KS, bool HP>
+template <int KS, bool HP, bool BV>
 static void launch_depth(bool small_depth, dim3 g, size_t lds, hipStream_t st, const KScene& ks, const KCam& kc,
                          const KParams& kp, const KWork& kw) {
   if (small_depth)
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
   else
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0, BV>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
 }
 
-static void launch_trace(uint32_t kinds, bool has_plane, bool small_depth, dim3 g, size_t lds, hipStream_t st,
-                         const KScene& ks, const KCam& kc, const KParams& kp, const KWork& kw) {
-  if (kinds == (1u << FR_AABB))
-    launch_depth<KS_AABB, false>(small_depth, g, lds, st, ks, kc, kp, kw);
-  else if (kinds == (1u << FR_SPHERE))
-    launch_depth<KS_SPHERE, false>(small_depth, g, lds, st, ks, kc, kp, kw);
-  else if (has_plane)
-    launch_depth<KS_ANY, true>(small_depth, g, lds, st, ks, kc, kp, kw);
-  else
-    launch_depth<KS_ANY, false>(small_depth, g, lds, st, ks, kc, kp, kw);
+// BVH kernels exist for plane-free scenes only (the plane's stale-record quirk needs
+// list order, so those scenes always take the in-order loop).
+static void launch_trace(uint32_t kinds, bool has_plane, bool bvh, bool small_depth, dim3 g, size_t lds,
+                         hipStream_t st, const KScene& ks, const KCam& kc, const KParams& kp, const KWork& kw) {
+  if (kinds == (1u << FR_AABB)) {
+    if (bvh)
+      launch_depth<KS_AABB, false, true>(small_depth, g, lds, st, ks, kc, kp, kw);
+    else
+      launch_depth<KS_AABB, false, false>(small_depth, g, lds, st, ks, kc, kp, kw);
+  } else if (kinds == (1u << FR_SPHERE)) {
+    if (bvh)
+      launch_depth<KS_SPHERE, false, true>(small_depth, g, lds, st, ks, kc, kp, kw);
+    else
+      launch_depth<KS_SPHERE, false, false>(small_depth, g, lds, st, ks, kc, kp, kw);
+  } else if (has_plane) {
+    launch_depth<KS_ANY, true, false>(small_depth, g, lds, st, ks, kc, kp, kw);
+  } else if (bvh) {
+    launch_depth<KS_ANY, false, true>(small_depth, g, lds, st, ks, kc, kp, kw);
+  } else {
+    launch_depth<KS_ANY, false, false>(small_depth, g, lds, st, ks, kc, kp, kw);
+  }
 }
 
 // Bytes of per-sample colours one pass may hold (FR_SAMPLE_BUFFER_GB, default 8).
@@ -965,6 +1042,12 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   ks.cls = reinterpret_cast<const uint32_t*>(b + dc->off_cls);
   ks.att = reinterpret_cast<const float4*>(b + dc->off_att);
   ks.n = dc->n;
+  // FR_BVH=0 forces the in-order loop (A/B and tests)
+  const char* bvh_env = getenv("FR_BVH");
+  const bool use_bvh = dc->bvh_n > 0 && !(bvh_env && strcmp(bvh_env, "0") == 0);
+  ks.bvh = reinterpret_cast<const float4*>(b + dc->off_bvh);
+  ks.bvh_order = reinterpret_cast<const uint32_t*>(b + dc->off_bvh_order);
+  ks.bvh_n = use_bvh ? dc->bvh_n : 0u;
   KCam kc{cam->position[0], cam->position[1], cam->position[2], cam->lower_left[0], cam->lower_left[1],
           cam->lower_left[2], cam->horizontal[0], cam->horizontal[1], cam->horizontal[2], cam->vertical[0],
           cam->vertical[1], cam->vertical[2], cam->u[0], cam->u[1], cam->u[2], cam->v[0], cam->v[1], cam->v[2],
@@ -1052,7 +1135,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
       const uint32_t blocks = static_cast<uint32_t>(want < 8ull * c->num_cus ? want : 8ull * c->num_cus);
       HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), c->stream));
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced], c->stream));
-      launch_trace(dc->kinds, dc->has_plane, small_depth, dim3(blocks), lds, c->stream, ks, kc, kp, kw);
+      launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, dim3(blocks), lds, c->stream, ks, kc, kp, kw);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced + 1], c->stream));
       ++traced;

@@ -18,6 +18,7 @@ from tests.golden import make_golden as G
 pytestmark = pytest.mark.gpu
 TOL = 1e-5  # north-star tolerance, f32 means per channel
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def assert_parity(mean, u8, st, omean, ou8, ocnt, rows=None):
@@ -352,3 +353,82 @@ def test_full_size_configs_on_row_subsets(gpu, cfg):
     # size-independent properties of the whole frame
     assert np.isfinite(mean).all() and (mean >= 0).all() and (mean <= 1).all()
     assert st["hits"] <= st["segments"] <= st["samples"] * (depth + 1)
+
+
+# ---- BVH (plane-free scenes of >= 64 primitives) ----------------
+
+def bvh_scene(seed, n=300, dup=True):
+    """Plane-free random scene of every bounded kind plus stubs; with dup, exact copies
+    of earlier primitives later in the list (and of later ones earlier), so exact-t ties
+    between list positions occur on every frame."""
+    r = np.random.default_rng(seed)
+    prims = []
+    for i in range(n):
+        kind = r.choice([S.SPHERE, S.SPHERE, S.AABB, S.OBB, S.TRIANGLE, S.TRIANGLE, S.STUB])
+        mat = int(r.integers(0, 5))
+        col = r.uniform(0.1, 1.0, 3)
+        fuzz = float(r.uniform(0, 1))
+        c = r.uniform(-6, 6, 3) + np.array([0, 0, -8.0])
+        if kind == S.SPHERE:
+            prims.append(S.sphere(c, r.uniform(0.1, 0.9), mat, col, fuzz))
+        elif kind == S.AABB:
+            hsz = r.uniform(0.05, 0.8, 3)
+            prims.append(S.prim(S.AABB, mat, col, fuzz, list(c - hsz) + list(c + hsz)))
+        elif kind == S.OBB:
+            q = r.standard_normal(4)
+            q /= np.linalg.norm(q)
+            ax = S.quat_axes(*q)
+            prims.append(S.prim(S.OBB, mat, col, fuzz, list(c) + list(ax[0]) + list(ax[1]) + list(ax[2])
+                                + list(r.uniform(0.05, 0.8, 3))))
+        elif kind == S.TRIANGLE:
+            v = [list(c + r.uniform(-1.0, 1.0, 3)) for _ in range(3)]
+            prims.append(S.prim(S.TRIANGLE, mat, col, fuzz, v[0] + v[1] + v[2]))
+        else:
+            prims.append(S.prim(S.STUB, mat, col, fuzz))
+    if dup:
+        for j in r.integers(0, n, 20):
+            q = dict(prims[int(j)])
+            q["material"] = int(r.integers(0, 4))  # same geometry, other material: the winner is visible
+            q["color"] = np.asarray(r.uniform(0.1, 1.0, 3), dtype=np.float32)
+            if r.uniform() < 0.5:
+                prims.append(q)
+            else:
+                prims.insert(int(r.integers(0, int(j) + 1)), q)
+    prims.append(S.sphere((0.0, -1000.5, -1.0), 1000.0, 0, (0.5, 0.5, 0.5), 0.0))
+    return prims
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_bvh_matches_list_order_loop(gpu, seed, monkeypatch):
+    w, h, spp, depth = 48, 32, 3, 8
+    prims = bvh_scene(seed)
+    sc = gpu.Scene.from_prims(prims)
+    cam = gpu.camera_new(w, h)
+    gpu.camera_orbit(cam, (0.3 * seed, 0.05 * seed, 1.5))
+    ocam = O.camera_new(w, h)
+    O.camera_orbit(ocam, (0.3 * seed, 0.05 * seed, 1.5))
+    mean, u8, st = gpu.render(sc, cam, w, h, spp, depth, seed=77 + seed)
+    omean, ou8, ocnt, _ = O.render(prims, ocam, w, h, spp, depth, seed=77 + seed, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    monkeypatch.setenv("FR_BVH", "0")  # the in-order loop gives the same bits
+    mean0, u80, st0 = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=77 + seed)
+    assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
+
+
+def test_bvh_generator_10k_spheres_small(gpu):
+    """C5's scene (tools/gen_scene.py --count 10000 --mesh sphere) at a size the oracle's
+    brute-force loop finishes quickly."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_scene", os.path.join(ROOT, "tools", "gen_scene.py"))
+    gs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gs)
+    text = gs.dumps(gs.generator_scene(10000, "sphere"))
+    w, h, spp, depth = 48, 27, 2, 8
+    sc = gpu.Scene.from_json(text, w, h)
+    assert len(sc) == 10000
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
+    prims, (frm, at, vup, fov) = S.load_json(text)
+    cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
+    omean, ou8, ocnt, _ = O.render(prims, cam, w, h, spp, depth, threads=16)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    assert st["hits"] > 0
