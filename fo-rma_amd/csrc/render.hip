@@ -113,6 +113,7 @@ struct KParams {
   uint32_t tiles_magic, tiles_shift;  // x / n_tiles = fastdiv(x, tiles_magic, tiles_shift)
   float rW, rH;                       // RN(1 / W), RN(1 / H) (host IEEE division)
   uint32_t row_magic, row_shift;      // x / tiles_per_row = fastdiv(x, row_magic, row_shift)
+  uint32_t band_h;                    // FR_FLAG_MT_BANDS: rows per band, H / 4 (tracer.rs:87)
 };
 
 // Unsigned 32-bit division by the invariant n_tiles: q = (t + ((x - t) >> s1)) >> s2 with
@@ -270,7 +271,7 @@ enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 // amdgpu_num_sgpr caps the scalar registers (MI355X_MICROARCH.md "Residency and
 // cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
 // admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
-template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH>
+template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) void trace_kernel(
     KScene sc, KCam cam, KParams kp, KWork kw) {
   // LDS: [attenuation rgb, n_att entries][stack: MAXD ? MAXD x kBlock u16 : max_depth x kBlock u32]
@@ -319,7 +320,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // pending o = hit point and d = scatter base ((p + n), or reflect(unit(d), n) for metal)
   V3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
   V3 sn{0.0f, 0.0f, 0.0f};  // metal: normal
-  float sfuzz = 0.0f, fx = 0.0f, fy = 0.0f;
+  float sfuzz = 0.0f, fx = 0.0f, fy = 0.0f, vofs = 0.0f;
   bool smetal = false;
   uint32_t sbest = 0, q = 0, s = 0, s_end = 0, nseg = 0, nhit = 0;
   float* out = kw.samples;                               // colour slot of the current sample
@@ -359,13 +360,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         continue;
       }
       uint32_t b, x, y;
-      if (item_xy(kp, item, b, q, x, y)) {
+      bool ok = item_xy(kp, item, b, q, x, y);
+      uint32_t yrow = kp.H - y;  // tracer.rs:171-172: v = ((H - y) + r) / H
+      if (MT) {
+        // render_mt (tracer.rs:86-103): band k from the top is thread t_id = 3 - k;
+        // v = ((t_height - y_band) + r) / H + t_id * 0.25; rows past 4 * t_height unused
+        const uint32_t k = kp.band_h ? y / kp.band_h : 4u;
+        ok = ok && k < 4u;
+        yrow = kp.band_h - (y - k * kp.band_h);
+        vofs = static_cast<float>(3u - k) * 0.25f;
+      }
+      if (ok) {
         rng = rng_seed(kp.seed, y * kp.W + x, b);  // this block's stream
         s = b * kBlockSamples;
         out = kw.samples + 3 * (static_cast<size_t>(s - s_pass) * kp.P + q);
         s_end = min(s + kBlockSamples, kp.spp);
         fx = static_cast<float>(x);
-        fy = static_cast<float>(kp.H - y);  // tracer.rs:171-172
+        fy = static_cast<float>(yrow);
         need_jit = true;
         need_item = false;
       }
@@ -378,6 +389,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       const float r1 = rng_f32(rng);
       d.x = div_rn(fx + r0, fW, kp.rW);  // (fx + r0) / fW, numerator +0 or in [2^-24, 2^32]
       d.y = div_rn(fy + r1, fH, kp.rH);
+      if (MT) d.y = d.y + vofs;  // render_mt's band offset (tracer.rs:103)
       need = NEED_LENS;
       need_jit = false;
     }
@@ -652,12 +664,28 @@ __global__ __launch_bounds__(256) void sum_kernel(KParams kp, const float* __res
   if (q >= kp.P) return;
   uint32_t x, y;
   if (!slot_xy(kp, q, x, y)) return;
+  const bool mt = (kp.flags & FR_FLAG_MT_BANDS) != 0;
+  if (mt && !(kp.band_h && y / kp.band_h < 4u)) {  // rows render_mt never fills stay 0
+    if (last) {
+      const size_t idx = (static_cast<size_t>(y) * kp.W + x) * 3u;
+      for (int ch = 0; ch < 3; ++ch) {
+        out_mean[idx + ch] = 0.0f;
+        out_u8[idx + ch] = 0;
+      }
+    }
+    return;
+  }
   V3 sum = first ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
   const uint32_t s0 = kp.b0 * kBlockSamples;
   const uint32_t s1 = min((kp.b0 + kp.nb) * kBlockSamples, kp.spp);
+  const float fspp = static_cast<float>(kp.spp);
   for (uint32_t s = s0; s < s1; ++s) {
     const float* c = samples + 3 * (static_cast<size_t>(s - s0) * kp.P + q);
-    sum = add(sum, V3{c[0], c[1], c[2]});
+    if (mt)  // save_image_mt (tracer.rs:140-145): acc += (sqrt(c) * 255) as u8 / sample
+      sum = add(sum, V3{static_cast<float>(to_u8(c[0])) / fspp, static_cast<float>(to_u8(c[1])) / fspp,
+                        static_cast<float>(to_u8(c[2])) / fspp});
+    else
+      sum = add(sum, V3{c[0], c[1], c[2]});
   }
   if (!last) {
     running[3 * q] = sum.x;
@@ -665,8 +693,17 @@ __global__ __launch_bounds__(256) void sum_kernel(KParams kp, const float* __res
     running[3 * q + 2] = sum.z;
     return;
   }
-  const V3 mean = divs(sum, static_cast<float>(kp.spp));  // tracer.rs:177
   const size_t idx = (static_cast<size_t>(y) * kp.W + x) * 3u;
+  if (mt) {  // tracer.rs:148-155: `pixels_acc as u8`
+    out_mean[idx + 0] = sum.x;
+    out_mean[idx + 1] = sum.y;
+    out_mean[idx + 2] = sum.z;
+    out_u8[idx + 0] = as_u8_trunc(sum.x);
+    out_u8[idx + 1] = as_u8_trunc(sum.y);
+    out_u8[idx + 2] = as_u8_trunc(sum.z);
+    return;
+  }
+  const V3 mean = divs(sum, static_cast<float>(kp.spp));  // tracer.rs:177
   out_mean[idx + 0] = mean.x;
   out_mean[idx + 1] = mean.y;
   out_mean[idx + 2] = mean.z;
@@ -900,20 +937,26 @@ struct fr_ctx {
 // Picks the specialisation: single-kind scenes (all boxes, all spheres) drop the
 // per-primitive kind switch; HAS_PLANE adds the stale-record bookkeeping; small depth
 // uses the u16 stack with the unrolled unwind.
-template <int KS, bool HP, bool BV>
+template <int KS, bool HP, bool BV, bool MT = false>
 static void launch_depth(bool small_depth, dim3 g, size_t lds, hipStream_t st, const KScene& ks, const KCam& kc,
                          const KParams& kp, const KWork& kw) {
   if (small_depth)
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV, MT>), g, dim3(kBlock), lds, st, ks, kc, kp,
+                       kw);
   else
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0, BV>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0, BV, MT>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
 }
 
 // BVH kernels exist for plane-free scenes only (the plane's stale-record quirk needs
 // list order, so those scenes always take the in-order loop).
 static void launch_trace(uint32_t kinds, bool has_plane, bool bvh, bool small_depth, dim3 g, size_t lds,
                          hipStream_t st, const KScene& ks, const KCam& kc, const KParams& kp, const KWork& kw) {
-  if (kinds == (1u << FR_AABB)) {
+  if (kp.flags & FR_FLAG_MT_BANDS) {  // save_image_mt: the general kernels, in-order loop
+    if (has_plane)
+      launch_depth<KS_ANY, true, false, true>(small_depth, g, lds, st, ks, kc, kp, kw);
+    else
+      launch_depth<KS_ANY, false, false, true>(small_depth, g, lds, st, ks, kc, kp, kw);
+  } else if (kinds == (1u << FR_AABB)) {
     if (bvh)
       launch_depth<KS_AABB, false, true>(small_depth, g, lds, st, ks, kc, kp, kw);
     else
@@ -1064,6 +1107,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   kp.shard_count = p->shard_count;
   kp.flags = p->flags;
   kp.tiles_per_row = (p->width + 7u) / 8u;
+  kp.band_h = p->height / 4u;
   const uint32_t strips = (p->height + kStripRows - 1) / kStripRows;
   const uint32_t my_strips =
       strips > p->shard_index ? (strips - p->shard_index + p->shard_count - 1) / p->shard_count : 0u;

@@ -396,4 +396,11 @@ FR_HD uint8_t to_u8(float c) {
   return static_cast<uint8_t>(s);
 }
 
+// Rust `f32 as u8` of a value already in byte units: NaN -> 0, saturating, truncation
+FR_HD uint8_t as_u8_trunc(float v) {
+  if (!(v > 0.0f)) return 0;
+  if (v >= 255.0f) return 255;
+  return static_cast<uint8_t>(v);
+}
+
 }  // namespace fr

@@ -31,6 +31,7 @@ FR_OK, FR_EARG, FR_EPARSE, FR_EHIP, FR_ENODEV, FR_ENOMEM = 0, -1, -2, -3, -4, -5
 FR_SPHERE, FR_PLANE, FR_AABB, FR_OBB, FR_STUB, FR_TRIANGLE = 0, 1, 2, 3, 4, 5
 FR_LAMBERTIAN, FR_METAL, FR_DIELECTRIC, FR_LIGHT = 0, 1, 2, 3
 FR_FLAG_WRITE_U8 = 1
+FR_FLAG_MT_BANDS = 2  # save_image_mt semantics (forma_rt.h)
 MAX_DEPTH = 50  # tracer.rs:10
 DEFAULT_SEED = 0x5EED
 
@@ -358,11 +359,11 @@ def scene_path(name):
 # ---- rendering ----------------------------------------------------------------
 
 def make_params(width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, shard_index=0, shard_count=1,
-                write_u8=True):
+                write_u8=True, mt_bands=False):
     p = FrParams()
     p.width, p.height, p.spp, p.max_depth, p.seed = width, height, spp, max_depth, seed
     p.strip_rows, p.shard_index, p.shard_count = 8, shard_index, shard_count
-    p.flags = FR_FLAG_WRITE_U8 if write_u8 else 0
+    p.flags = (FR_FLAG_WRITE_U8 if write_u8 else 0) | (FR_FLAG_MT_BANDS if mt_bands else 0)
     return p
 
 
@@ -402,13 +403,14 @@ class RenderContext:
 
 
 def render(scene, cam, width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, device=0, shard_index=0,
-           shard_count=1, n_gpus=1):
+           shard_count=1, n_gpus=1, mt_bands=False):
     """Render on the GPU. Returns (mean[H,W,3] f32, u8[H,W,3], stats). Rows outside the
-    shard are NaN / 0. n_gpus > 1 row-shards the whole image across devices 0..n-1."""
+    shard are NaN / 0. n_gpus > 1 row-shards the whole image across devices 0..n-1.
+    mt_bands: save_image_mt semantics (mean then holds the u8 average, 0..255)."""
     mean = np.full((height, width, 3), np.nan, dtype=np.float32)
     u8 = np.zeros((height, width, 3), dtype=np.uint8)
     st = FrStats()
-    p = make_params(width, height, spp, max_depth, seed, shard_index, shard_count)
+    p = make_params(width, height, spp, max_depth, seed, shard_index, shard_count, mt_bands=mt_bands)
     fm, fu = mean.ctypes.data_as(C.POINTER(C.c_float)), u8.ctypes.data_as(C.POINTER(C.c_uint8))
     if n_gpus > 1:
         check(lib().fr_render_hip_multi(scene._h, C.byref(cam), C.byref(p), n_gpus, fm, fu, C.byref(st)))
@@ -465,6 +467,17 @@ def write_png(path, rgb8):
         f.write(chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0)))
         f.write(chunk(b"IDAT", zlib.compress(raw, 6)))
         f.write(chunk(b"IEND", b""))
+
+
+def save_image_mt(model, sample, path="out/basic_mt.png", max_depth=MAX_DEPTH):
+    """tracer.rs:136-158: `sample` passes of render_mt (4 row bands over the plain simple
+    scene, scenes::get_simple_scene, with the model's camera), each pass gamma-corrected
+    to u8, the u8 frames averaged and truncated, PNG."""
+    simple = Scene.builtin(0, model.width, model.height)
+    acc, u8, stats = render(simple, model.scene.camera, model.width, model.height, sample, max_depth, model.seed,
+                            model.device, mt_bands=True)
+    write_png(path, u8)
+    return acc, u8, stats
 
 
 def save_image(model, sample, path="out/basic.png", max_depth=MAX_DEPTH):

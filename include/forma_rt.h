@@ -71,6 +71,12 @@ extern "C" {
 
 /* flags for fr_params.flags */
 #define FR_FLAG_WRITE_U8 1u /* also write the u8 image (tracer.rs:177-184) */
+/* save_image_mt (tracer.rs:83-158): 4 row bands of H/4 rows, v = ((H/4 - y_band) + r)/H
+   + band * 0.25, each sample gamma-corrected and quantised to u8, the u8 values averaged
+   as acc += u8 / spp in f32 and truncated; rows past 4 * (H/4) stay 0. mean_rgb then
+   holds acc (0..255). Render the plain simple scene (fr_scene_builtin 0) with
+   max_depth 50 to match the reference call. */
+#define FR_FLAG_MT_BANDS 2u
 
 /*
  * One primitive, in the order it is tested (list order decides ties, tracer.rs:195-200).

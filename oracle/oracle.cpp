@@ -785,4 +785,62 @@ int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, ui
   return int64_t(rows.size());
 }
 
+// save_image_mt (tracer.rs:136-158) over render_mt (tracer.rs:83-134), in their
+// shape: `sample` passes; each pass renders 4 row bands of t_height = H/4 rows (band
+// t_id covers image rows from the top in the order 3, 2, 1, 0) with
+// v = ((t_height - y) + r) / H + t_id * 0.25, gamma-corrects and quantises every pixel
+// to u8, and the passes are averaged as acc += u8 / sample in f32, then `as u8`. Rows
+// past 4 * t_height are never written (0). A pixel's passes draw from the build's
+// streams exactly as save_image's samples do (block s / 16 of (seed, pixel)), so the
+// per-pixel stream state is carried from pass to pass.
+int oracle_render_mt(const or_prim* prims, uint32_t n, const or_camera* cam, uint32_t width, uint32_t height,
+                     uint32_t sample, uint32_t max_depth, uint64_t seed, float* out_acc, uint8_t* out_u8,
+                     or_counters* counters) {
+  if (!cam || width == 0 || height == 0 || sample == 0 || !out_acc || !out_u8) return -1;
+  const auto objects = build(prims, n);
+  Camera camera;
+  camera.from_c(cam);
+  const uint32_t NTHREADS = 4;
+  const uint32_t t_height = height / NTHREADS;
+  const float t_offset = 1.0f / float(NTHREADS);
+  std::vector<float> acc(size_t(width) * height * 3, 0.0f);
+  std::vector<Rng> streams(size_t(width) * height, Rng(seed, 0, 0));
+  Counters cnt;
+  for (uint32_t pass = 0; pass < sample; ++pass) {
+    std::vector<uint8_t> pixels(size_t(width) * height * 3, 0);  // render_mt's result, bands stacked
+    for (uint32_t t_id = 0; t_id < NTHREADS; ++t_id) {
+      for (uint32_t y = 0; y < t_height; ++y) {
+        for (uint32_t x = 0; x < width; ++x) {
+          const uint32_t row = (NTHREADS - 1 - t_id) * t_height + y;  // ids sorted descending (:122-127)
+          const uint32_t pixel = row * width + x;
+          Rng& rng = streams[pixel];
+          if (pass % 16 == 0) rng = Rng(seed, pixel, pass / 16);
+          const float u = (float(x) + rng.gen_f32()) / float(width);
+          float v = (float(t_height - y) + rng.gen_f32()) / float(height);
+          v += float(t_id) * t_offset;
+          const Ray ray = camera.get_ray(u, v, rng);
+          const Vec3 color = get_color(ray, objects, 0, max_depth, rng, cnt);
+          const size_t index = size_t(pixel) * 3;
+          pixels[index] = as_u8(sqrtf(color.r()) * 255.0f);
+          pixels[index + 1] = as_u8(sqrtf(color.g()) * 255.0f);
+          pixels[index + 2] = as_u8(sqrtf(color.b()) * 255.0f);
+        }
+      }
+    }
+    const size_t filled = size_t(width) * t_height * NTHREADS * 3;
+    for (size_t k = 0; k < filled; ++k) acc[k] += float(pixels[k]) / float(sample);  // :141-144
+  }
+  for (size_t k = 0; k < acc.size(); ++k) {
+    out_acc[k] = acc[k];
+    out_u8[k] = as_u8(acc[k]);
+  }
+  if (counters) {
+    counters->segments = cnt.segments;
+    counters->hits = cnt.hits;
+    counters->scatters = cnt.scatters;
+    counters->samples = uint64_t(width) * t_height * NTHREADS * sample;
+  }
+  return 0;
+}
+
 }  // extern "C"

@@ -144,3 +144,22 @@ def render(prims, cam, width, height, spp, max_depth, seed=0x5EED, shard_index=0
         raise ValueError("oracle_render: bad arguments")
     return mean, u8, {"segments": cnt.segments, "hits": cnt.hits, "samples": cnt.samples,
                       "scatters": cnt.scatters}, int(rows)
+
+
+def render_mt(prims, cam, width, height, sample, max_depth=50, seed=0x5EED):
+    """save_image_mt semantics (tracer.rs:136-158): returns (acc[H,W,3] f32, u8[H,W,3], counters)."""
+    L = lib()
+    if not getattr(L.oracle_render_mt, "argtypes", None):
+        L.oracle_render_mt.argtypes = [C.POINTER(OrPrim), C.c_uint32, C.POINTER(OrCamera), C.c_uint32, C.c_uint32,
+                                       C.c_uint32,
+                                       C.c_uint32, C.c_uint64, C.POINTER(C.c_float), C.POINTER(C.c_uint8),
+                                       C.POINTER(OrCounters)]
+    acc = np.zeros((height, width, 3), dtype=np.float32)
+    u8 = np.zeros((height, width, 3), dtype=np.uint8)
+    cnt = OrCounters()
+    rc = L.oracle_render_mt(prims_to_c(prims), len(prims), C.byref(cam),
+                            width, height, sample, max_depth, seed, acc.ctypes.data_as(C.POINTER(C.c_float)),
+                            u8.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(cnt))
+    if rc != 0:
+        raise ValueError("oracle_render_mt: bad arguments")
+    return acc, u8, {"segments": cnt.segments, "hits": cnt.hits, "samples": cnt.samples, "scatters": cnt.scatters}

@@ -432,3 +432,25 @@ def test_bvh_generator_10k_spheres_small(gpu):
     omean, ou8, ocnt, _ = O.render(prims, cam, w, h, spp, depth, threads=16)
     assert_parity(mean, u8, st, omean, ou8, ocnt)
     assert st["hits"] > 0
+
+
+# ---- save_image_mt (tracer.rs:83-158) ---------------------------------------------
+
+@pytest.mark.parametrize("which,w,h,sample", [(0, 32, 18, 3), (0, 40, 24, 1), (2, 36, 22, 20), (0, 16, 3, 2)])
+def test_save_image_mt_bands_match_oracle(gpu, which, w, h, sample):
+    """4 row bands of H/4 rows with the band offset in v, per-pass u8, u8 average; rows past
+    4*(H/4) stay 0 (h = 3: no band rows at all)."""
+    sc = gpu.Scene.builtin(which, w, h)
+    acc, u8, st = gpu.render(sc, sc.camera, w, h, sample, 50, seed=0x5EED, mt_bands=True)
+    oacc, ou8, ocnt = O.render_mt(S.BUILTIN[which](), O.camera_new(w, h), w, h, sample, 50, 0x5EED)
+    assert np.array_equal(acc.view(np.uint32), oacc.view(np.uint32))
+    assert np.array_equal(u8, ou8)
+    assert (st["segments"], st["hits"]) == (ocnt["segments"], ocnt["hits"])
+    assert not u8[4 * (h // 4):].any()
+
+
+def test_save_image_mt_writes_png(gpu, tmp_path):
+    m = gpu.create_model(24, 16)
+    out = tmp_path / "basic_mt.png"
+    acc, u8, st = gpu.save_image_mt(m, 2, str(out))
+    assert out.read_bytes()[:8] == b"\x89PNG\r\n\x1a\n" and u8.shape == (16, 24, 3)
