@@ -36,6 +36,7 @@ __device__ unsigned long long g_fr_diag_rus[2];
   } while (0)
 // per-wave start/end (s_memrealtime, 100 MHz) for the residency-over-time profile
 __device__ unsigned long long g_fr_wave_times[2 * 65536];
+__device__ unsigned long long g_fr_wave_drain[65536];  // first drained claim of the wave
 #define FR_LENS_TRY() FR_DIAG_TRY(g_fr_diag_lens)
 #define FR_RUS_TRY() FR_DIAG_TRY(g_fr_diag_rus)
 #endif
@@ -64,7 +65,12 @@ constexpr uint32_t kSmallDepth = 8;
 #define FR_BLOCK_SAMPLES 16  // RNG contract: one stream per 16-sample block (oracle.cpp agrees)
 #endif
 constexpr uint32_t kBlockSamples = FR_BLOCK_SAMPLES;  // samples per RNG stream (numerics contract)
-constexpr uint32_t kBatch = 64;         // work items claimed per global atomic (one tile, one block)  // max_depth <= 8: u16 index stack, unrolled unwind
+#ifndef FR_BATCH
+#define FR_BATCH 64
+#endif
+// work items reserved per step of the global counter (a claim reserves whole steps)
+constexpr uint32_t kBatch = FR_BATCH;
+static_assert(kBatch >= 1 && kBatch <= 64 && (kBatch & (kBatch - 1)) == 0, "kBatch: power of two <= 64");
 
 // ABI layout, mirrored by ctypes (forma_rt.py) and the Rust binding
 static_assert(sizeof(fr_prim) == 88, "fr_prim layout");
@@ -177,7 +183,21 @@ __device__ __forceinline__ RecRef rec_at(const float4* base, uint32_t i) {
   return RecRef{(cfloat*)(reinterpret_cast<uintptr_t>(base)) + 16u * i};
 }
 
-constexpr uint32_t kAttLds = 1024;  // attenuation table entries staged in LDS
+// Raw buffer loads (SGPR resource over a uniform base pointer). Used where an LDS and a
+// global read of the same value sit on two sides of a uniform branch: a buffer load
+// cannot be merged with the LDS read into one generic (flat) load.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ float4 buf_load4(const void* base, uint32_t byte_off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(buf_rsrc(base), byte_off, 0, 0));
+}
+__device__ __forceinline__ uint32_t buf_load1(const void* base, uint32_t byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(base), byte_off, 0, 0);
+}
+
+constexpr uint32_t kAttLds = 1024;  // attenuation/class entries staged in LDS (16 B each)
+constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for small scenes
 
 // FR_DIAG builds count, per phase, wave-level trips (one per SIMT pass of the wave)
 // and lane-level work, to measure SIMT efficiency. Never enabled in the product.
@@ -274,21 +294,24 @@ enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) void trace_kernel(
     KScene sc, KCam cam, KParams kp, KWork kw) {
-  // LDS: [attenuation rgb, n_att entries][stack: MAXD ? MAXD x kBlock u16 : max_depth x kBlock u32]
+  // LDS: [n_att x (attenuation rgb, scatter class bits)][n_rec x 64-B record]
+  //      [stack: MAXD ? MAXD x kBlock u16 : max_depth x kBlock u32]
+  // Staging the winner's data keeps per-lane global gathers off the shading path.
   extern __shared__ uint32_t lds[];
   __shared__ uint32_t wq_next[kBlock / 64], wq_end[kBlock / 64];  // per-wave item batch
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
-  float* att_lds = reinterpret_cast<float*>(lds);
-  uint32_t* stack = lds + n_att * 3u;
+  const uint32_t n_rec = sc.n <= kRecLds ? sc.n : 0u;
+  float4* att_lds = reinterpret_cast<float4*>(lds);
+  float4* rec_lds = att_lds + n_att;
+  uint32_t* stack = reinterpret_cast<uint32_t*>(rec_lds + 4u * n_rec);
   uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wave = tid >> 6;
   for (uint32_t i = tid; i < n_att; i += kBlock) {
     const float4 a = sc.att[i];
-    att_lds[3 * i + 0] = a.x;
-    att_lds[3 * i + 1] = a.y;
-    att_lds[3 * i + 2] = a.z;
+    att_lds[i] = make_float4(a.x, a.y, a.z, __uint_as_float(sc.cls[i]));
   }
+  for (uint32_t i = tid; i < 4u * n_rec; i += kBlock) rec_lds[i] = sc.rec[i];
   if (lane == 0) {
     wq_next[wave] = 0;
     wq_end[wave] = 0;
@@ -297,7 +320,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   __shared__ uint32_t dg[DG_N];
   if (tid < DG_N) dg[tid] = 0;
   const uint32_t gw = blockIdx.x * (kBlock / 64u) + wave;
-  if (lane == 0 && gw < 65536) g_fr_wave_times[2 * gw] = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && gw < 65536) {
+    g_fr_wave_times[2 * gw] = __builtin_amdgcn_s_memrealtime();
+    g_fr_wave_drain[gw] = ~0ull;
+  }
 #endif
   __syncthreads();
 
@@ -346,16 +372,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       const uint32_t next = wq_next[wave], end = wq_end[wave];
       const uint32_t avail = end - next;
       uint32_t base = 0;
-      if (n > avail) {
-        if (r == 0) base = atomicAdd(kw.queue, static_cast<uint32_t>(kBatch));
+      // the lanes past the wave's batch need `want` items: reserve whole kBatch steps
+      const uint32_t grab = n > avail ? (n - avail + kBatch - 1u) & ~(kBatch - 1u) : 0u;
+      if (grab) {
+        if (r == 0) base = atomicAdd(kw.queue, grab);
         base = __builtin_amdgcn_readfirstlane(base);
       }
       const uint32_t item = r < avail ? next + r : base + (r - avail);
       if (r == 0) {
-        wq_next[wave] = n > avail ? base + (n - avail) : next + n;
-        if (n > avail) wq_end[wave] = base + static_cast<uint32_t>(kBatch);
+        wq_next[wave] = grab ? base + (n - avail) : next + n;
+        if (grab) wq_end[wave] = base + grab;
       }
       if (item >= kp.n_items) {
+#ifdef FR_DIAG
+        if (gw < 65536) atomicMin(&g_fr_wave_drain[gw], static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+#endif
         active = false;  // queue drained
         continue;
       }
@@ -542,9 +573,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         if (depth < kp.max_depth) {
           // the shared HitRecord: normal of the winner at its own t; p = point_at(last t written)
           const V3 pw = add(o, scl(closest, d));
-          const float4* rb = sc.rec + 4 * best;
-          const uint32_t kb = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(rb[3].w);
-          const float4 b0 = rb[0], b1 = rb[1];
+          // the winner's record and class: LDS when staged (n_rec / n_att are uniform;
+          // separate branches keep LDS and global reads in their own address spaces)
+          float4 b0, b1, b2, b3;
+          if (n_rec) {
+            const float4* rb = rec_lds + 4 * best;
+            b0 = rb[0];
+            b1 = rb[1];
+            b2 = rb[2];
+            b3 = rb[3];
+          } else {
+            const uint32_t off = 64u * static_cast<uint32_t>(best);
+            b0 = buf_load4(sc.rec, off);
+            b1 = buf_load4(sc.rec, off + 16u);
+            b2 = buf_load4(sc.rec, off + 32u);
+            b3 = buf_load4(sc.rec, off + 48u);
+          }
+          const uint32_t c = n_att ? __float_as_uint(att_lds[best].w) : buf_load1(sc.cls, 4u * best);
+          const uint32_t kb = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(b3.w);
           V3 n;
           if (kb == FR_AABB) {
             n = slab_normal(slab3(xyz(b0), xyz(b1), o, inv), closest, d);
@@ -554,16 +600,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
             n = scl(-1.0f, xyz(b1));
           } else if (kb == FR_TRIANGLE) {
             // precomputed winding normal, turned to face the ray except for dielectric
-            n = xyz(rb[3]);
-            if (sc.cls[best] != SC_DIELECTRIC && dot(n, d) > 0.0f) n = scl(-1.0f, n);
+            n = xyz(b3);
+            if (c != SC_DIELECTRIC && dot(n, d) > 0.0f) n = scl(-1.0f, n);
           } else {
-            const float4 b2 = rb[2], b3 = rb[3];
             const ObbFrame f = obb_frame(xyz(b0), xyz(b1), xyz(b2), xyz(b3), o, d);
             const Slab sl = slab3(V3{-b0.w, -b1.w, -b2.w}, V3{b0.w, b1.w, b2.w}, f.ol, f.inv);
             n = obb_normal(xyz(b1), xyz(b2), xyz(b3), sl, closest, f.dl);
           }
           const V3 p = HAS_PLANE ? add(o, scl(t_last, d)) : pw;
-          const uint32_t c = sc.cls[best];
           if (c == SC_DIELECTRIC) {
             // one draw, no rejection loop (sphere.rs:107-145)
             const V3 nd = scatter_dielectric(d, n, rng);
@@ -606,7 +650,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
             DIAG_WAVE(DG_UNW_W);
             DIAG_LANE(DG_UNW_L);
             const uint32_t pi = hstack[j * kBlock + tid];
-            col = mul(V3{att_lds[3 * pi], att_lds[3 * pi + 1], att_lds[3 * pi + 2]}, col);
+            col = mul(xyz(att_lds[pi]), col);
           }
         }
       } else if (MAXD > 0) {
@@ -616,7 +660,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       } else if (n_att) {
         for (int j = static_cast<int>(depth) - 1; j >= 0; --j) {
           const uint32_t pi = stack[j * kBlock + tid];
-          col = mul(V3{att_lds[3 * pi], att_lds[3 * pi + 1], att_lds[3 * pi + 2]}, col);
+          col = mul(xyz(att_lds[pi]), col);
         }
       } else {
         for (int j = static_cast<int>(depth) - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
@@ -1152,7 +1196,8 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   const size_t stack_bytes = small_depth ? kSmallDepth * kBlock * sizeof(uint16_t)
                                          : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
                                                sizeof(uint32_t);
-  const size_t lds = n_att * 3 * sizeof(float) + stack_bytes;
+  const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
+  const size_t lds = n_att * 16 + n_rec * 64 + stack_bytes;
   KWork kw;
   kw.queue = reinterpret_cast<uint32_t*>(c->d_cnt + 31);
   kw.samples = c->d_samples;
@@ -1229,6 +1274,9 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
     if (const char* path = getenv("FR_DIAG_TIMES")) {
       std::vector<unsigned long long> wt(2 * 65536);
       HIPCHK(hipMemcpyFromSymbol(wt.data(), HIP_SYMBOL(g_fr_wave_times), wt.size() * 8));
+      std::vector<unsigned long long> wd(65536);
+      HIPCHK(hipMemcpyFromSymbol(wd.data(), HIP_SYMBOL(g_fr_wave_drain), wd.size() * 8));
+      wt.insert(wt.end(), wd.begin(), wd.end());
       if (FILE* f = fopen(path, "wb")) {
         fwrite(wt.data(), 8, wt.size(), f);
         fclose(f);

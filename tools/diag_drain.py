@@ -1,0 +1,19 @@
+"""Tail analysis from an FR_DIAG FR_DIAG_TIMES file: per wave start/end stamps plus the
+first drained claim (100 MHz s_memrealtime)."""
+import sys
+import numpy as np
+
+raw = np.fromfile(sys.argv[1], dtype=np.uint64)
+t = raw[: 2 * 65536].reshape(-1, 2)
+dr = raw[2 * 65536: 3 * 65536]
+n = int((t[:, 1] > 0).sum())
+t, dr = t[:n].astype(np.float64), dr[:n]
+t0 = t[:, 0].min()
+s, e = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0
+ok = dr != np.uint64(2 ** 64 - 1)
+d = (dr[ok].astype(np.float64) - t0) / 100.0
+print(f"waves {n}, kernel {e.max()/1e3:.3f} ms; first drain {d.min()/1e3:.3f} ms, median drain {np.median(d)/1e3:.3f} ms")
+tail = e[ok] - d
+print(f"per-wave end - first drained claim: mean {tail.mean()/1e3:.3f} p50 {np.median(tail)/1e3:.3f} "
+      f"p90 {np.percentile(tail, 90)/1e3:.3f} max {tail.max()/1e3:.3f} ms")
+print(f"kernel end - first drain anywhere: {(e.max() - d.min())/1e3:.3f} ms")
