@@ -292,7 +292,12 @@ enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 // cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
 // admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
 template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) void trace_kernel(
+#ifdef FR_WAVES_PER_EU
+#define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU, FR_WAVES_PER_EU)))
+#else
+#define FR_OCC_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) FR_OCC_ATTR void trace_kernel(
     KScene sc, KCam cam, KParams kp, KWork kw) {
   // LDS: [n_att x (attenuation rgb, scatter class bits)][n_rec x 64-B record]
   //      [stack: MAXD ? MAXD x kBlock u16 : max_depth x kBlock u32]
@@ -327,8 +332,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #endif
   __syncthreads();
 
-  const V3 cpos{cam.px, cam.py, cam.pz}, cllc{cam.lx, cam.ly, cam.lz}, chor{cam.hx, cam.hy, cam.hz};
-  const V3 cver{cam.vx, cam.vy, cam.vz}, cu{cam.ux, cam.uy, cam.uz}, cv{cam.bx, cam.by, cam.bz};
+
   const float fW = static_cast<float>(kp.W), fH = static_cast<float>(kp.H);
   const uint32_t s_pass = kp.b0 * kBlockSamples;
 
@@ -445,7 +449,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       if (acc) {
         if (!sph) {
           // Camera::get_ray (camera.rs:62-72)
-          const V3 rd = scl(cam.lens, V3{px, py, 0.0f});
+          const KCam& cm = cam;
+          const V3 cpos{cm.px, cm.py, cm.pz}, cllc{cm.lx, cm.ly, cm.lz}, chor{cm.hx, cm.hy, cm.hz};
+          const V3 cver{cm.vx, cm.vy, cm.vz}, cu{cm.ux, cm.uy, cm.uz}, cv{cm.bx, cm.by, cm.bz};
+          const V3 rd = scl(cm.lens, V3{px, py, 0.0f});
           const V3 off = add(scl(rd.x, cu), scl(rd.y, cv));
           const float u = d.x, v = d.y;
           o = add(cpos, off);
