@@ -80,6 +80,8 @@ struct Builder {
   std::vector<BvhNode>& nodes;
   float pad;
 
+  uint32_t order_base = 0;  // leaf indices are absolute positions in the shared order array
+
   // Emits the subtree over items[begin, end) at nodes.size(); returns its node index.
   uint32_t build(uint32_t begin, uint32_t end) {
     const uint32_t at = static_cast<uint32_t>(nodes.size());
@@ -100,7 +102,7 @@ struct Builder {
       if (n > kBvhLeafMax) {           // no useful split (coincident centroids): halve by index
         mid = begin + n / 2;
       } else {
-        nodes[at].leaf = (n << 24) | begin;
+        nodes[at].leaf = (n << 24) | (order_base + begin);
         nodes[at].escape = static_cast<uint32_t>(nodes.size());
         return at;
       }
@@ -167,31 +169,72 @@ struct Builder {
   }
 };
 
-}  // namespace
+float scene_abs_max(const std::vector<fr_prim>& prims) {
+  float m = 0.0f;
+  for (const fr_prim& p : prims) {
+    Box3 b;
+    if (!prim_bounds(p, b)) continue;
+    for (int k = 0; k < 3; ++k) m = std::max(m, std::max(fabsf(b.lo[k]), fabsf(b.hi[k])));
+  }
+  return m;
+}
 
-bool build_bvh(const std::vector<fr_prim>& prims, std::vector<BvhNode>& nodes, std::vector<uint32_t>& order) {
-  nodes.clear();
-  order.clear();
+bool build_range(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end, float pad,
+                 std::vector<BvhNode>& nodes, std::vector<uint32_t>& order) {
   std::vector<Item> items;
-  items.reserve(prims.size());
-  float scene_abs = 0.0f;
-  for (uint32_t i = 0; i < prims.size(); ++i) {
+  items.reserve(end - begin);
+  for (uint32_t i = begin; i < end; ++i) {
     Item it;
     if (!prim_bounds(prims[i], it.box)) continue;
-    for (int k = 0; k < 3; ++k) {
-      it.c[k] = 0.5f * (it.box.lo[k] + it.box.hi[k]);
-      scene_abs = std::max(scene_abs, std::max(fabsf(it.box.lo[k]), fabsf(it.box.hi[k])));
-    }
+    for (int k = 0; k < 3; ++k) it.c[k] = 0.5f * (it.box.lo[k] + it.box.hi[k]);
     it.index = i;
     items.push_back(it);
   }
   if (items.empty()) return false;
+  // Leaf indices must fit the node's 24-bit field.
+  if (order.size() + items.size() >= (1u << 24)) return false;
+  Builder b{items, nodes, pad};
+  b.order_base = static_cast<uint32_t>(order.size());
+  b.build(0, static_cast<uint32_t>(items.size()));
+  for (const Item& it : items) order.push_back(it.index);
+  return true;
+}
+
+}  // namespace
+
+bool build_bvh(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end, std::vector<BvhNode>& nodes,
+               std::vector<uint32_t>& order) {
   // The cull must never reject a primitive whose own test accepts a hit: pad every box
   // by a margin far above the f32 error of a root or a slab distance at scene scale.
-  Builder b{items, nodes, 1e-4f * scene_abs + 1e-4f};
-  b.build(0, static_cast<uint32_t>(items.size()));
-  order.resize(items.size());
-  for (size_t i = 0; i < items.size(); ++i) order[i] = items[i].index;
+  const float pad = 1e-4f * scene_abs_max(prims) + 1e-4f;
+  return build_range(prims, begin, end, pad, nodes, order);
+}
+
+bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& segs, std::vector<BvhNode>& nodes,
+                    std::vector<uint32_t>& order) {
+  segs.clear();
+  nodes.clear();
+  order.clear();
+  const uint32_t n = static_cast<uint32_t>(prims.size());
+  uint32_t planes = 0;
+  for (const fr_prim& p : prims) planes += p.kind == FR_PLANE;
+  if (n < kBvhMinPrims || planes > kBvhMaxPlanes) return false;
+  const float pad = 1e-4f * scene_abs_max(prims) + 1e-4f;
+  uint32_t i = 0;
+  while (i < n) {
+    if (prims[i].kind == FR_PLANE) {
+      segs.push_back(BvhSegment{1u, 0u, 0u, i});
+      ++i;
+      continue;
+    }
+    uint32_t j = i;
+    while (j < n && prims[j].kind != FR_PLANE) ++j;
+    const uint32_t first = static_cast<uint32_t>(nodes.size());
+    if (!build_range(prims, i, j, pad, nodes, order) && nodes.size() != first) return false;
+    const uint32_t last = static_cast<uint32_t>(nodes.size());
+    if (last > first) segs.push_back(BvhSegment{0u, first, last, 0u});
+    i = j;
+  }
   return true;
 }
 

@@ -30,10 +30,28 @@ static_assert(sizeof(BvhNode) == 32, "BvhNode is two float4");
 constexpr uint32_t kBvhLeafMax = 4;      // primitives per leaf
 constexpr uint32_t kBvhMinPrims = 64;    // smaller scenes keep the in-order loop
 
-// Builds the BVH over prims (stubs are left out: they never hit). `order` receives the
-// primitive indices in leaf order. Returns false (and leaves both empty) if no
-// primitive can be bounded.
-bool build_bvh(const std::vector<fr_prim>& prims, std::vector<BvhNode>& nodes, std::vector<uint32_t>& order);
+// Builds the BVH over prims[begin, end) (stubs are left out: they never hit), appending
+// its nodes to `nodes` and its leaf primitive indices (global) to `order`; escape and
+// leaf indices are absolute. Returns false (appending nothing) if no primitive of the
+// range can be bounded.
+bool build_bvh(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end, std::vector<BvhNode>& nodes,
+               std::vector<uint32_t>& order);
+
+// The closest-hit list cut at its planes: runs of consecutive non-plane primitives (one
+// BVH each) and single planes, in list order. A plane hit ignores t_max and may leave
+// a stale record (plane.rs:24-44), so planes are tested one by one where they stand.
+struct BvhSegment {
+  uint32_t plane;       // 1: a plane, prims index `prim`; 0: a run with nodes [first, end)
+  uint32_t first, end;  // node range of the run's tree (end == first: nothing boundable)
+  uint32_t prim;
+};
+static_assert(sizeof(BvhSegment) == 16, "BvhSegment is one uint4");
+
+constexpr uint32_t kBvhMaxPlanes = 32;  // more planes: the in-order loop
+
+// Segments and trees for a scene; false if the scene is too small or has too many planes.
+bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& segs, std::vector<BvhNode>& nodes,
+                    std::vector<uint32_t>& order);
 
 }  // namespace fr
 

@@ -87,8 +87,9 @@ struct DeviceCopy {
   uint32_t kinds = 0;  // bit k set if a primitive of kind k is present
   size_t off_kind = 0, off_g0 = 0, off_g1 = 0, off_g2 = 0, off_g3 = 0, off_mat = 0, off_cls = 0, off_att = 0;
   size_t off_rec = 0;
-  size_t off_bvh = 0, off_bvh_order = 0;
-  uint32_t bvh_n = 0;  // BVH nodes (0 = in-order loop only)
+  size_t off_bvh = 0, off_bvh_order = 0, off_segs = 0;
+  uint32_t bvh_n = 0;   // BVH nodes (0 = in-order loop only)
+  uint32_t n_segs = 0;  // closest-hit segments: BVH runs and planes (bvh.h)
 };
 
 struct KScene {
@@ -105,8 +106,10 @@ struct KScene {
   const float4* __restrict__ att;   // attenuation rgb (colour, or 1 for light)
   const float4* __restrict__ bvh;   // BVH nodes, two float4 each (bvh.h), or null
   const uint32_t* __restrict__ bvh_order;  // primitive index of each leaf slot
+  const uint4* __restrict__ segs;   // BvhSegment list: runs (one tree each) and planes, in list order
   uint32_t n;
   uint32_t bvh_n;                   // node count (0: no BVH)
+  uint32_t n_segs;                  // segment count
 };
 
 struct KParams {
@@ -492,47 +495,67 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       float closest = FLT_MAX, t_last = 0.0f;
       int best = -1;
       if (BVH) {
-        // Threaded BVH walk (bvh.h), one node index per lane. A primitive's candidate t
-        // does not depend on t_max, so the list loop's winner is the least (t, index):
-        // a primitive listed before the current winner may also take an exact tie,
-        // tested with t_max one ulp above closest. Boxes are padded, so no primitive
-        // the list loop accepts is culled.
-        uint32_t ni = 0;
-        while (ni < sc.bvh_n) {
-          const float4 na = sc.bvh[2 * ni], nb = sc.bvh[2 * ni + 1];
-          const Slab sl = slab3(xyz(na), xyz(nb), o, inv);
-          const bool enter = (sl.tn <= sl.tf) & (sl.tf >= 0.001f) & (sl.tn <= closest);
-          const uint32_t leaf = __float_as_uint(nb.w);
-          if (enter && leaf) {
-            const uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
-            for (uint32_t kk = 0; kk < cnt; ++kk) {
-              const uint32_t i = sc.bvh_order[first + kk];
-              const float4* r = sc.rec + 4 * i;
-              const float tmax =
-                  static_cast<int>(i) < best ? __uint_as_float(__float_as_uint(closest) + 1u) : closest;
-              const uint32_t k = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(r[3].w);
-              float t = 0.0f;
-              bool h = false;
-              if (k == FR_SPHERE) {
-                const float4 g = r[0];
-                h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, tmax, t);
-              } else if (k == FR_AABB) {
-                h = slab_root(slab3(xyz(r[0]), xyz(r[1]), o, inv), 0.001f, tmax, t);
-              } else if (k == FR_TRIANGLE) {
-                h = tri_root(xyz(r[0]), xyz(r[1]), xyz(r[2]), o, d, 0.001f, tmax, t);
-              } else if (k == FR_OBB) {
-                const float4 a = r[0], b = r[1], c = r[2], e = r[3];
-                const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
-                h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, tmax, t);
-              }
-              if (h) {
-                closest = t;
-                best = static_cast<int>(i);
-              }
+        // The list cut at its planes (bvh.h), walked in list order: each plane tested
+        // where it stands, each run of other primitives through its own threaded tree,
+        // one node index per lane. A primitive's candidate t does not depend on t_max,
+        // so a run's effect is the least (t, index) of the run below `closest`: a
+        // primitive listed before the current winner may take an exact tie, tested with
+        // t_max one ulp above closest. Boxes are padded, so no primitive the list loop
+        // accepts is culled.
+        typedef __attribute__((address_space(4))) const uint32_t cu32;
+        for (uint32_t sg = 0; sg < sc.n_segs; ++sg) {
+          const cu32* sp = (cu32*)(reinterpret_cast<uintptr_t>(sc.segs)) + 4u * __builtin_amdgcn_readfirstlane(sg);
+          if (HAS_PLANE && sp[0]) {
+            const uint32_t i = sp[3];
+            const RecRef r4 = rec_at(sc.rec, i);  // scalar loads
+            float t = 0.0f;
+            const int r = plane_test(xyz(r4[0]), xyz(r4[1]), xyz(r4[2]), o, d, 0.001f, closest, t);
+            if (r) t_last = t;
+            if (r == 2) {
+              closest = t;
+              best = static_cast<int>(i);
             }
-            ni = __float_as_uint(na.w);
-          } else {
-            ni = enter ? ni + 1u : __float_as_uint(na.w);
+            continue;
+          }
+          uint32_t ni = sp[1];
+          const uint32_t nend = sp[2];
+          while (ni < nend) {
+            const float4 na = sc.bvh[2 * ni], nb = sc.bvh[2 * ni + 1];
+            const Slab sl = slab3(xyz(na), xyz(nb), o, inv);
+            const bool enter = (sl.tn <= sl.tf) & (sl.tf >= 0.001f) & (sl.tn <= closest);
+            const uint32_t leaf = __float_as_uint(nb.w);
+            if (enter && leaf) {
+              const uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
+              for (uint32_t kk = 0; kk < cnt; ++kk) {
+                const uint32_t i = sc.bvh_order[first + kk];
+                const float4* r = sc.rec + 4 * i;
+                const float tmax =
+                    static_cast<int>(i) < best ? __uint_as_float(__float_as_uint(closest) + 1u) : closest;
+                const uint32_t k = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(r[3].w);
+                float t = 0.0f;
+                bool h = false;
+                if (k == FR_SPHERE) {
+                  const float4 g = r[0];
+                  h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, tmax, t);
+                } else if (k == FR_AABB) {
+                  h = slab_root(slab3(xyz(r[0]), xyz(r[1]), o, inv), 0.001f, tmax, t);
+                } else if (k == FR_TRIANGLE) {
+                  h = tri_root(xyz(r[0]), xyz(r[1]), xyz(r[2]), o, d, 0.001f, tmax, t);
+                } else if (k == FR_OBB) {
+                  const float4 a = r[0], b = r[1], c = r[2], e = r[3];
+                  const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
+                  h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, tmax, t);
+                }
+                if (h) {
+                  closest = t;
+                  best = static_cast<int>(i);
+                  if (HAS_PLANE) t_last = t;
+                }
+              }
+              ni = __float_as_uint(na.w);
+            } else {
+              ni = enter ? ni + 1u : __float_as_uint(na.w);
+            }
           }
         }
       }
@@ -841,12 +864,15 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   }
   const uint32_t n = static_cast<uint32_t>(s->prims.size());
   const size_t m = n ? n : 1;  // never hand the kernel a null array
-  // BVH for plane-free scenes of kBvhMinPrims or more (bvh.h)
-  bool any_plane = false;
-  for (const fr_prim& p : s->prims) any_plane |= p.kind == FR_PLANE;
+  // BVH runs between planes for scenes of kBvhMinPrims or more (bvh.h)
+  std::vector<BvhSegment> bvh_segs;
   std::vector<BvhNode> bvh_nodes;
   std::vector<uint32_t> bvh_order;
-  if (!any_plane && n >= kBvhMinPrims) build_bvh(s->prims, bvh_nodes, bvh_order);
+  if (!build_segments(s->prims, bvh_segs, bvh_nodes, bvh_order)) {
+    bvh_segs.clear();
+    bvh_nodes.clear();
+    bvh_order.clear();
+  }
   size_t off = 0;
   c->off_kind = off;
   off = align_up(off + m * 4, 256);
@@ -870,12 +896,16 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   off = align_up(off + (bvh_nodes.size() ? bvh_nodes.size() : 1) * sizeof(BvhNode), 256);
   c->off_bvh_order = off;
   off = align_up(off + (bvh_order.size() ? bvh_order.size() : 1) * 4, 256);
+  c->off_segs = off;
+  off = align_up(off + (bvh_segs.size() ? bvh_segs.size() : 1) * sizeof(BvhSegment), 256);
   std::vector<unsigned char> host(off, 0);
   if (!bvh_nodes.empty()) {
     memcpy(&host[c->off_bvh], bvh_nodes.data(), bvh_nodes.size() * sizeof(BvhNode));
     memcpy(&host[c->off_bvh_order], bvh_order.data(), bvh_order.size() * 4);
   }
+  if (!bvh_segs.empty()) memcpy(&host[c->off_segs], bvh_segs.data(), bvh_segs.size() * sizeof(BvhSegment));
   c->bvh_n = static_cast<uint32_t>(bvh_nodes.size());
+  c->n_segs = static_cast<uint32_t>(bvh_segs.size());
   for (uint32_t i = 0; i < n; ++i) {
     const fr_prim& p = s->prims[i];
     uint32_t kind = p.kind;
@@ -998,8 +1028,8 @@ static void launch_depth(bool small_depth, dim3 g, size_t lds, hipStream_t st, c
     hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0, BV, MT>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
 }
 
-// BVH kernels exist for plane-free scenes only (the plane's stale-record quirk needs
-// list order, so those scenes always take the in-order loop).
+// BVH kernels walk the list's segments (bvh.h); scenes with planes use the general
+// kernel, which tests each plane in list order between the runs.
 static void launch_trace(uint32_t kinds, bool has_plane, bool bvh, bool small_depth, dim3 g, size_t lds,
                          hipStream_t st, const KScene& ks, const KCam& kc, const KParams& kp, const KWork& kw) {
   if (kp.flags & FR_FLAG_MT_BANDS) {  // save_image_mt: the general kernels, in-order loop
@@ -1018,7 +1048,10 @@ static void launch_trace(uint32_t kinds, bool has_plane, bool bvh, bool small_de
     else
       launch_depth<KS_SPHERE, false, false>(small_depth, g, lds, st, ks, kc, kp, kw);
   } else if (has_plane) {
-    launch_depth<KS_ANY, true, false>(small_depth, g, lds, st, ks, kc, kp, kw);
+    if (bvh)
+      launch_depth<KS_ANY, true, true>(small_depth, g, lds, st, ks, kc, kp, kw);
+    else
+      launch_depth<KS_ANY, true, false>(small_depth, g, lds, st, ks, kc, kp, kw);
   } else if (bvh) {
     launch_depth<KS_ANY, false, true>(small_depth, g, lds, st, ks, kc, kp, kw);
   } else {
@@ -1142,6 +1175,8 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   ks.bvh = reinterpret_cast<const float4*>(b + dc->off_bvh);
   ks.bvh_order = reinterpret_cast<const uint32_t*>(b + dc->off_bvh_order);
   ks.bvh_n = use_bvh ? dc->bvh_n : 0u;
+  ks.segs = reinterpret_cast<const uint4*>(b + dc->off_segs);
+  ks.n_segs = use_bvh ? dc->n_segs : 0u;
   KCam kc{cam->position[0], cam->position[1], cam->position[2], cam->lower_left[0], cam->lower_left[1],
           cam->lower_left[2], cam->horizontal[0], cam->horizontal[1], cam->horizontal[2], cam->vertical[0],
           cam->vertical[1], cam->vertical[2], cam->u[0], cam->u[1], cam->u[2], cam->v[0], cam->v[1], cam->v[2],

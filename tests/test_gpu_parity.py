@@ -357,7 +357,7 @@ def test_full_size_configs_on_row_subsets(gpu, cfg):
 
 # ---- BVH (plane-free scenes of >= 64 primitives) ----------------
 
-def bvh_scene(seed, n=300, dup=True):
+def bvh_scene(seed, n=300, dup=True, planes=0):
     """Plane-free random scene of every bounded kind plus stubs; with dup, exact copies
     of earlier primitives later in the list (and of later ones earlier), so exact-t ties
     between list positions occur on every frame."""
@@ -394,14 +394,22 @@ def bvh_scene(seed, n=300, dup=True):
                 prims.append(q)
             else:
                 prims.insert(int(r.integers(0, int(j) + 1)), q)
+    for _ in range(planes):  # planes cut the list into BVH runs (bvh.h)
+        o = np.zeros(3)
+        o[r.integers(0, 3)] = r.choice([-1.0, 1.0])
+        if r.uniform() < 0.3:
+            o = r.standard_normal(3)
+        c = r.uniform(-6, 6, 3) + np.array([0, 0, -8.0])
+        prims.insert(int(r.integers(0, len(prims) + 1)),
+                     S.plane(c, o, r.uniform(0.5, 4, 3), int(r.integers(0, 5)), r.uniform(0.1, 1.0, 3), 0.3))
     prims.append(S.sphere((0.0, -1000.5, -1.0), 1000.0, 0, (0.5, 0.5, 0.5), 0.0))
     return prims
 
 
-@pytest.mark.parametrize("seed", range(4))
-def test_bvh_matches_list_order_loop(gpu, seed, monkeypatch):
+@pytest.mark.parametrize("seed,planes", [(0, 0), (1, 0), (2, 0), (3, 0), (4, 1), (5, 3), (6, 12)])
+def test_bvh_matches_list_order_loop(gpu, seed, planes, monkeypatch):
     w, h, spp, depth = 48, 32, 3, 8
-    prims = bvh_scene(seed)
+    prims = bvh_scene(seed, planes=planes)
     sc = gpu.Scene.from_prims(prims)
     cam = gpu.camera_new(w, h)
     gpu.camera_orbit(cam, (0.3 * seed, 0.05 * seed, 1.5))
