@@ -218,7 +218,10 @@ bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& 
   const uint32_t n = static_cast<uint32_t>(prims.size());
   uint32_t planes = 0;
   for (const fr_prim& p : prims) planes += p.kind == FR_PLANE;
-  if (n < kBvhMinPrims || planes > kBvhMaxPlanes) return false;
+  float cost = 0.0f;
+  for (const fr_prim& p : prims)
+    cost += p.kind == FR_TRIANGLE ? 2.5f : p.kind == FR_OBB ? 2.0f : (p.kind == FR_STUB ? 0.0f : 1.0f);
+  if (n < kBvhMinPrims || cost < kBvhMinCost || planes > kBvhMaxPlanes) return false;
   const float pad = 1e-4f * scene_abs_max(prims) + 1e-4f;
   uint32_t i = 0;
   while (i < n) {

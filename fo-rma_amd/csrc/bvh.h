@@ -29,6 +29,10 @@ static_assert(sizeof(BvhNode) == 32, "BvhNode is two float4");
 
 constexpr uint32_t kBvhLeafMax = 4;      // primitives per leaf
 constexpr uint32_t kBvhMinPrims = 64;    // smaller scenes keep the in-order loop
+// The in-order loop (wave-uniform, scalar loads) beats a divergent per-lane walk until
+// a segment's tests cost enough: weight box / sphere 1, oriented box 2, triangle 2.5
+// (measured: 217 boxes 93 ms in order vs 124 ms BVH; 156 triangles 49 ms vs 19 ms).
+constexpr float kBvhMinCost = 300.0f;
 
 // Builds the BVH over prims[begin, end) (stubs are left out: they never hit), appending
 // its nodes to `nodes` and its leaf primitive indices (global) to `order`; escape and

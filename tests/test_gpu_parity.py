@@ -357,7 +357,13 @@ def test_full_size_configs_on_row_subsets(gpu, cfg):
 
 # ---- BVH (plane-free scenes of >= 64 primitives) ----------------
 
-def bvh_scene(seed, n=300, dup=True, planes=0):
+def bvh_cost(prims):
+    """bvh.cpp's weighted test cost (the BVH is used at >= 300)."""
+    w = {S.TRIANGLE: 2.5, S.OBB: 2.0, S.STUB: 0.0}
+    return sum(w.get(p["kind"], 1.0) for p in prims)
+
+
+def bvh_scene(seed, n=400, dup=True, planes=0):
     """Plane-free random scene of every bounded kind plus stubs; with dup, exact copies
     of earlier primitives later in the list (and of later ones earlier), so exact-t ties
     between list positions occur on every frame."""
@@ -410,6 +416,7 @@ def bvh_scene(seed, n=300, dup=True, planes=0):
 def test_bvh_matches_list_order_loop(gpu, seed, planes, monkeypatch):
     w, h, spp, depth = 48, 32, 3, 8
     prims = bvh_scene(seed, planes=planes)
+    assert bvh_cost(prims) >= 300  # so the product takes the BVH path
     sc = gpu.Scene.from_prims(prims)
     cam = gpu.camera_new(w, h)
     gpu.camera_orbit(cam, (0.3 * seed, 0.05 * seed, 1.5))
