@@ -81,6 +81,7 @@ EXPORTS = (
     "fr_camera_init", "fr_camera_look", "fr_camera_orbit", "fr_camera_translate", "fr_update_delta",
     "fr_ctx_create", "fr_ctx_free", "fr_ctx_render", "fr_ctx_sync", "fr_ctx_download", "fr_ctx_device_buffers",
     "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_recip",
+    "fr_post_process", "fr_post_process_device", "fr_rgb_to_rgba_device",
 )
 
 _lib = None
@@ -136,6 +137,11 @@ def lib():
     L.fr_render_hip_multi.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
     L.fr_selftest_ops.argtypes = [C.c_int, C.c_int, f3, f3, C.c_uint32, f3]
     L.fr_selftest_rng.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+    if hasattr(L, "fr_post_process"):  # absent from A/B builds of older sources
+        L.fr_post_process.argtypes = [C.c_int, P(C.c_int), C.c_uint32, C.c_float, C.c_uint32, C.c_uint32,
+                                      P(C.c_uint8), P(C.c_uint8)]
+        L.fr_post_process_device.argtypes = [vp, P(C.c_int), C.c_uint32, C.c_float, C.c_uint32, C.c_uint32, vp, vp]
+        L.fr_rgb_to_rgba_device.argtypes = [vp, vp, vp, C.c_size_t]
     if hasattr(L, "fr_selftest_recip"):  # absent from A/B builds of older sources
         L.fr_selftest_recip.argtypes = [C.c_int, C.c_uint64, C.c_uint64, P(C.c_uint64), P(C.c_uint32)]
     _lib = L
@@ -390,6 +396,12 @@ class RenderContext:
                                     u8.ctypes.data_as(C.POINTER(C.c_uint8))))
         return mean, u8
 
+    def device_buffers(self):
+        """(d_mean_rgb, d_rgb8) device addresses of the last render's full-image outputs."""
+        dm, du = C.c_void_p(), C.c_void_p()
+        check(lib().fr_ctx_device_buffers(self._h, C.byref(dm), C.byref(du)))
+        return dm.value, du.value
+
     def close(self):
         if self._h and self._h.value:
             lib().fr_ctx_free(self._h)
@@ -417,6 +429,27 @@ def render(scene, cam, width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEE
     else:
         check(lib().fr_render_hip(scene._h, C.byref(cam), C.byref(p), device, fm, fu, C.byref(st)))
     return mean, u8, st.as_dict()
+
+
+# ---- post-process effects (src/shaders/compute/*.wgsl) -------------------------
+
+EFFECTS = ["none", "noise", "pixelate", "invert_color", "wave", "interlace", "flipaxis", "grayscale", "step",
+           "watercolor", "chromostereopsis", "anaglyph"]  # shader_utils.rs:58-88 order and names
+
+
+def post_process(rgba, effects, time=0.0, device=0):
+    """Run the effect chain (post_processor.rs:101-129) on an [H, W, 4] uint8 image (or an
+    [H, W, 3] one, given alpha 255). `effects`: ids or names. Returns a new [H, W, 4] array."""
+    img = np.ascontiguousarray(rgba, dtype=np.uint8)
+    if img.shape[-1] == 3:
+        img = np.concatenate([img, np.full(img.shape[:2] + (1,), 255, np.uint8)], -1)
+    ids = [EFFECTS.index(e) if isinstance(e, str) else int(e) for e in effects]
+    h, w, _ = img.shape
+    out = np.empty_like(img)
+    arr = (C.c_int * max(1, len(ids)))(*ids)
+    check(lib().fr_post_process(device, arr, len(ids), float(time), w, h,
+                                img.ctypes.data_as(C.POINTER(C.c_uint8)), out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return out
 
 
 # ---- tracer.rs operator API ---------------------------------------------------

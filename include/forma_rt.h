@@ -192,6 +192,33 @@ int fr_render_hip(fr_scene* scene, const fr_camera* cam, const fr_params* params
 int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* params, int n_gpus,
                         float* mean_rgb, uint8_t* rgb8, fr_stats* stats);
 
+/* ---- post-process effects (src/shaders/compute/<name>.comp.wgsl, rendering/post_processor.rs:101-129) ----
+   Effect ids in shader_utils.rs:58-71 order. Images are RGBA8, row-major, W*H*4 bytes.
+   Effects run in the given order, each reading the previous one's output, exactly like
+   the reference's ping-pong between its two intermediate textures; `time` is the
+   control uniform's values[0] (post_processor.rs:114, seconds), used by noise.
+   Implementation-defined WGSL details are fixed in DESIGN.md §4.10. */
+#define FR_FX_NONE 0
+#define FR_FX_NOISE 1
+#define FR_FX_PIXELATE 2
+#define FR_FX_INVERT_COLOR 3
+#define FR_FX_WAVE 4
+#define FR_FX_INTERLACE 5
+#define FR_FX_FLIP_AXIS 6
+#define FR_FX_GRAYSCALE 7
+#define FR_FX_STEP 8
+#define FR_FX_WATERCOLOR 9
+#define FR_FX_CHROMOSTEREOPSIS 10
+#define FR_FX_ANAGLYPH 11
+/* Host buffers in and out (synchronous). */
+int fr_post_process(int device, const int* effects, uint32_t n_effects, float time, uint32_t width, uint32_t height,
+                    const uint8_t* rgba_in, uint8_t* rgba_out);
+/* Device buffers, in place on d_rgba (d_scratch: another W*H*4 bytes), async on `stream`. */
+int fr_post_process_device(void* stream, const int* effects, uint32_t n_effects, float time, uint32_t width,
+                           uint32_t height, uint8_t* d_rgba, uint8_t* d_scratch);
+/* Device RGB8 (a render's u8 output) -> RGBA8 with alpha 255, async on `stream`. */
+int fr_rgb_to_rgba_device(void* stream, const uint8_t* d_rgb, uint8_t* d_rgba, size_t pixels);
+
 /* ---- diagnostics ---- */
 /* Run the device f32/RNG primitives on n inputs (op codes in DESIGN.md §7); used by the
    parity tests to show the GPU arithmetic is bit-identical to the host's. */
