@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <chrono>
+#include <cmath>
 #include <thread>
 
 #include "bvh.h"
@@ -90,6 +91,7 @@ struct DeviceCopy {
   size_t off_bvh = 0, off_bvh_order = 0, off_segs = 0;
   uint32_t bvh_n = 0;   // BVH nodes (0 = in-order loop only)
   uint32_t n_segs = 0;  // closest-hit segments: BVH runs and planes (bvh.h)
+  bool att_nonneg = true;  // every attenuation component finite and >= +0 (no -0)
 };
 
 struct KScene {
@@ -110,6 +112,7 @@ struct KScene {
   uint32_t n;
   uint32_t bvh_n;                   // node count (0: no BVH)
   uint32_t n_segs;                  // segment count
+  uint32_t att_nonneg;              // every attenuation component finite and >= +0
 };
 
 struct KParams {
@@ -671,12 +674,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       DIAG_WAVE(DG_END_W);
       DIAG_LANE(DG_END_L);
       V3 col = term;
+      // An absorbed path (terminal colour +0) stays +0 through any chain of finite,
+      // non-negative attenuations: skip its unwind (sc.att_nonneg is the host's check).
+      const bool zero_term = (__float_as_uint(term.x) | __float_as_uint(term.y) | __float_as_uint(term.z)) == 0u;
+      const int udepth = sc.att_nonneg && zero_term ? 0 : static_cast<int>(depth);
       // n_att is wave-uniform: one unwind per attenuation source keeps LDS reads as
       // ds_read (a merged pointer would become flat loads)
       if (MAXD > 0 && n_att) {
 #pragma unroll
         for (int j = MAXD - 1; j >= 0; --j) {
-          if (j < static_cast<int>(depth)) {
+          if (j < udepth) {
             DIAG_WAVE(DG_UNW_W);
             DIAG_LANE(DG_UNW_L);
             const uint32_t pi = hstack[j * kBlock + tid];
@@ -686,14 +693,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       } else if (MAXD > 0) {
 #pragma unroll
         for (int j = MAXD - 1; j >= 0; --j)
-          if (j < static_cast<int>(depth)) col = mul(xyz(sc.att[hstack[j * kBlock + tid]]), col);
+          if (j < udepth) col = mul(xyz(sc.att[hstack[j * kBlock + tid]]), col);
       } else if (n_att) {
-        for (int j = static_cast<int>(depth) - 1; j >= 0; --j) {
+        for (int j = udepth - 1; j >= 0; --j) {
           const uint32_t pi = stack[j * kBlock + tid];
           col = mul(xyz(att_lds[pi]), col);
         }
       } else {
-        for (int j = static_cast<int>(depth) - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
+        for (int j = udepth - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
       }
       out[0] = col.x;
       out[1] = col.y;
@@ -899,6 +906,7 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   c->off_segs = off;
   off = align_up(off + (bvh_segs.size() ? bvh_segs.size() : 1) * sizeof(BvhSegment), 256);
   std::vector<unsigned char> host(off, 0);
+  bool nonneg = true;
   if (!bvh_nodes.empty()) {
     memcpy(&host[c->off_bvh], bvh_nodes.data(), bvh_nodes.size() * sizeof(BvhNode));
     memcpy(&host[c->off_bvh_order], bvh_order.data(), bvh_order.size() * 4);
@@ -906,6 +914,7 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   if (!bvh_segs.empty()) memcpy(&host[c->off_segs], bvh_segs.data(), bvh_segs.size() * sizeof(BvhSegment));
   c->bvh_n = static_cast<uint32_t>(bvh_nodes.size());
   c->n_segs = static_cast<uint32_t>(bvh_segs.size());
+  c->att_nonneg = nonneg;
   for (uint32_t i = 0; i < n; ++i) {
     const fr_prim& p = s->prims[i];
     uint32_t kind = p.kind;
@@ -953,6 +962,8 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
     memcpy(&host[c->off_mat + 16 * i], &mat, 16);
     memcpy(&host[c->off_cls + 4 * i], &cls, 4);
     memcpy(&host[c->off_att + 16 * i], &att, 16);
+    for (float a : {att.x, att.y, att.z})
+      if (!(a >= 0.0f) || std::signbit(a) || !std::isfinite(a)) nonneg = false;
     memcpy(&g[3].w, &kind, 4);  // kind bits in g3.w
     memcpy(&host[c->off_rec + 64 * i], g, 64);
   }
@@ -1177,6 +1188,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   ks.bvh_n = use_bvh ? dc->bvh_n : 0u;
   ks.segs = reinterpret_cast<const uint4*>(b + dc->off_segs);
   ks.n_segs = use_bvh ? dc->n_segs : 0u;
+  ks.att_nonneg = dc->att_nonneg ? 1u : 0u;
   KCam kc{cam->position[0], cam->position[1], cam->position[2], cam->lower_left[0], cam->lower_left[1],
           cam->lower_left[2], cam->horizontal[0], cam->horizontal[1], cam->horizontal[2], cam->vertical[0],
           cam->vertical[1], cam->vertical[2], cam->u[0], cam->u[1], cam->u[2], cam->v[0], cam->v[1], cam->v[2],

@@ -469,3 +469,21 @@ def test_save_image_mt_writes_png(gpu, tmp_path):
     out = tmp_path / "basic_mt.png"
     acc, u8, st = gpu.save_image_mt(m, 2, str(out))
     assert out.read_bytes()[:8] == b"\x89PNG\r\n\x1a\n" and u8.shape == (16, 24, 3)
+
+
+@pytest.mark.parametrize("colors", ["nonneg", "negative", "negzero"])
+def test_absorbed_paths_skip_unwind_only_when_exact(gpu, colors):
+    """An absorbed path's colour is +0 through finite non-negative attenuations; with a
+    negative or -0 attenuation component the product's zero sign depends on the chain,
+    so the unwind must run (sc.att_nonneg). Bits of the mean are compared."""
+    w, h, spp, depth = 40, 24, 3, 4
+    prims = random_scene(21)
+    if colors == "negative":
+        prims[1]["color"] = np.array([-0.5, 0.25, 0.75], np.float32)
+    elif colors == "negzero":
+        prims[1]["color"] = np.array([-0.0, 0.25, 0.75], np.float32)
+    sc = gpu.Scene.from_prims(prims)
+    mean, u8, st = gpu.render(sc, gpu.camera_new(w, h), w, h, spp, depth, seed=5)
+    omean, ou8, ocnt, _ = O.render(prims, O.camera_new(w, h), w, h, spp, depth, seed=5, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
