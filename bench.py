@@ -137,12 +137,12 @@ def cpu_baseline(budget_s=12.0):
     threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
     prims, (frm, at, vup, fov) = scene_ref.load_json(open(fr.scene_path(SCENE)).read())
     cam = oracle_py.camera_look(frm, at, vup, fov, 0.1, WIDTH, HEIGHT)
-    # calibrate on 4 rows, then size the sample to ~budget_s
-    step = HEIGHT // 4
+    # calibrate on two rows per thread (every thread busy), then size the sample to ~budget_s
+    step = max(1, HEIGHT // (2 * threads))
     t = time.perf_counter()
     _, _, cnt, rows = oracle_py.render(prims, cam, WIDTH, HEIGHT, SPP, DEPTH, SEED, row_step=step, threads=threads)
     dt = time.perf_counter() - t
-    per_row = dt / max(1, rows)
+    per_row = dt / max(1, rows)  # wall time per row with all threads working
     want_rows = max(threads, int(budget_s / max(per_row, 1e-6)))
     step = max(1, HEIGHT // want_rows)
     t = time.perf_counter()
