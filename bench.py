@@ -165,6 +165,9 @@ def main():
     a = ap.parse_args()
 
     rank, world, local = dist_env()
+    # rehearsal only: run every rank on one device (timing is then meaningless)
+    if os.environ.get("FR_BENCH_DEVICE") is not None:
+        local = int(os.environ["FR_BENCH_DEVICE"])
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
