@@ -1,17 +1,19 @@
 // render.hip — the gfx950 path-tracing megakernel and its host driver.
 //
 // Replaces cpu_ray_tracer/tracer.rs:160-219 (save_image + recursive get_color)
-// and the shapes/ hit/scatter code it calls. One lane owns one pixel for all of
-// its samples, so the per-pixel f32 sum runs in sample order exactly as
-// `col = col + get_color(...)` does (tracer.rs:170-175). A lane whose path ends
-// immediately starts its next sample (path regeneration), so no lane idles while
-// its wave still has work. The attenuation product is unwound right-to-left from
-// a per-lane LDS stack, reproducing the recursion's association
-// a0*(a1*(...*terminal)) bit for bit.
+// and the shapes/ hit/scatter code it calls. A persistent grid pulls work items
+// (one pixel's 16-sample RNG block) from a global counter; every lane holds one path
+// segment per loop iteration and a lane whose path ends starts its next sample at
+// once (path regeneration), so lanes never wait for each other's pixels. Each
+// sample's colour goes to a per-sample buffer that sum_kernel adds per pixel in
+// sample order, exactly as `col = col + get_color(...)` does (tracer.rs:170-175).
+// The attenuation product is unwound right-to-left from a per-lane LDS stack,
+// reproducing the recursion's association a0*(a1*(...*terminal)) bit for bit.
 //
-// Scene data is wave-uniform inside the closest-hit loop (every lane tests
-// primitive i at the same time): the kind switch is a scalar branch and the
-// geometry arrives by scalar loads. Layout and rooflines: DESIGN.md §4-§5.
+// Closest hit: small scenes test primitive i on every lane at once (wave-uniform:
+// the kind switch is a scalar branch, records arrive by scalar loads); large ones
+// walk a threaded BVH per lane, cut at the planes (bvh.h). Layout and rooflines:
+// DESIGN.md §4-§5.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdio.h>
@@ -86,7 +88,7 @@ struct DeviceCopy {
   uint32_t n = 0;
   bool has_plane = false;
   uint32_t kinds = 0;  // bit k set if a primitive of kind k is present
-  size_t off_kind = 0, off_g0 = 0, off_g1 = 0, off_g2 = 0, off_g3 = 0, off_mat = 0, off_cls = 0, off_att = 0;
+  size_t off_mat = 0, off_cls = 0, off_att = 0;
   size_t off_rec = 0;
   size_t off_bvh = 0, off_bvh_order = 0, off_segs = 0;
   uint32_t bvh_n = 0;   // BVH nodes (0 = in-order loop only)
@@ -98,11 +100,6 @@ struct KScene {
   // one 64-B record per primitive (g0..g3; kind in the bits of g3.w): one scalar
   // load brings a primitive into SGPRs in the closest-hit loop
   const float4* __restrict__ rec;
-  const uint32_t* __restrict__ kind;
-  const float4* __restrict__ g0;
-  const float4* __restrict__ g1;
-  const float4* __restrict__ g2;
-  const float4* __restrict__ g3;
   const float4* __restrict__ mat;   // colour rgb, fuzz
   const uint32_t* __restrict__ cls; // effective ScatterClass
   const float4* __restrict__ att;   // attenuation rgb (colour, or 1 for light)
@@ -881,16 +878,6 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
     bvh_order.clear();
   }
   size_t off = 0;
-  c->off_kind = off;
-  off = align_up(off + m * 4, 256);
-  c->off_g0 = off;
-  off = align_up(off + m * 16, 256);
-  c->off_g1 = off;
-  off = align_up(off + m * 16, 256);
-  c->off_g2 = off;
-  off = align_up(off + m * 16, 256);
-  c->off_g3 = off;
-  off = align_up(off + m * 16, 256);
   c->off_mat = off;
   off = align_up(off + m * 16, 256);
   c->off_cls = off;
@@ -954,11 +941,6 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
     const float4 mat = make_float4(p.color[0], p.color[1], p.color[2], p.fuzz);
     const float4 att = cls == SC_LIGHT ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
                                        : make_float4(p.color[0], p.color[1], p.color[2], 0.0f);
-    memcpy(&host[c->off_kind + 4 * i], &kind, 4);
-    memcpy(&host[c->off_g0 + 16 * i], &g[0], 16);
-    memcpy(&host[c->off_g1 + 16 * i], &g[1], 16);
-    memcpy(&host[c->off_g2 + 16 * i], &g[2], 16);
-    memcpy(&host[c->off_g3 + 16 * i], &g[3], 16);
     memcpy(&host[c->off_mat + 16 * i], &mat, 16);
     memcpy(&host[c->off_cls + 4 * i], &cls, 4);
     memcpy(&host[c->off_att + 16 * i], &att, 16);
@@ -969,7 +951,6 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   }
   if (n == 0) {
     const uint32_t stub = FR_STUB;
-    memcpy(&host[c->off_kind], &stub, 4);
     memcpy(&host[c->off_rec + 60], &stub, 4);
   }
   HIPCHK(hipMalloc(&c->blob, off));
@@ -1171,11 +1152,6 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   KScene ks;
   const char* b = static_cast<const char*>(dc->blob);
   ks.rec = reinterpret_cast<const float4*>(b + dc->off_rec);
-  ks.kind = reinterpret_cast<const uint32_t*>(b + dc->off_kind);
-  ks.g0 = reinterpret_cast<const float4*>(b + dc->off_g0);
-  ks.g1 = reinterpret_cast<const float4*>(b + dc->off_g1);
-  ks.g2 = reinterpret_cast<const float4*>(b + dc->off_g2);
-  ks.g3 = reinterpret_cast<const float4*>(b + dc->off_g3);
   ks.mat = reinterpret_cast<const float4*>(b + dc->off_mat);
   ks.cls = reinterpret_cast<const uint32_t*>(b + dc->off_cls);
   ks.att = reinterpret_cast<const float4*>(b + dc->off_att);
