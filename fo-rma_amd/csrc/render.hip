@@ -991,8 +991,12 @@ struct fr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_start = nullptr;
   std::vector<hipEvent_t> ev_trace;  // start/stop pairs around each pass's trace kernel
+  std::vector<hipEvent_t> ev_sum;    // end of each pass's sum kernel
+  // Pass pipeline: traces alternate between `stream` and `stream2`,
+  // sums run on `stream_sum`, so a pass's sum and tail overlap the next pass's trace.
+  hipStream_t stream2 = nullptr, stream_sum = nullptr;
   int passes = 0;
   float* d_mean = nullptr;
   uint8_t* d_u8 = nullptr;
@@ -1106,6 +1110,9 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
   if (c->num_cus <= 0) c->num_cus = 256;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream_sum, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_cnt, 32 * sizeof(unsigned long long)) != hipSuccess) {
     fr_ctx_free(c);
     return set_error(FR_EHIP, "fr_ctx_create: event/counter allocation failed");
@@ -1124,6 +1131,10 @@ void fr_ctx_free(fr_ctx* c) {
   if (c->d_samples) (void)hipFree(c->d_samples);
   if (c->d_running) (void)hipFree(c->d_running);
   for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_sum) (void)hipEventDestroy(e);
+  if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+  if (c->stream2) (void)hipStreamSynchronize(c->stream2), (void)hipStreamDestroy(c->stream2);
+  if (c->stream_sum) (void)hipStreamSynchronize(c->stream_sum), (void)hipStreamDestroy(c->stream_sum);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -1190,23 +1201,37 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   fastdiv_magic(kp.n_tiles, kp.tiles_magic, kp.tiles_shift);
   fastdiv_magic(kp.tiles_per_row, kp.row_magic, kp.row_shift);
   const uint32_t nblocks = (p->spp + kBlockSamples - 1) / kBlockSamples;
-  // passes: as many sample blocks per pass as the sample buffer holds
+  // Passes of nb_pass blocks each. With more than one pass the sample buffer holds two
+  // pass slots (a pass traces into one while the previous pass's sum reads the other).
+  // FR_PIPELINE (default 2) asks for at least that many passes; the buffer budget
+  // (FR_SAMPLE_BUFFER_GB) may force more.
   const size_t per_block = static_cast<size_t>(kp.P) * kBlockSamples * 3 * sizeof(float);
-  uint32_t nb_pass = per_block ? static_cast<uint32_t>(sample_buffer_cap() / per_block) : nblocks;
+  uint32_t want_passes = 2;
+  if (const char* e = getenv("FR_PIPELINE")) want_passes = static_cast<uint32_t>(atoi(e) > 0 ? atoi(e) : 1);
+  uint32_t passes_u = nblocks ? (want_passes < nblocks ? want_passes : nblocks) : 0u;
+  uint32_t nb_pass = passes_u ? (nblocks + passes_u - 1) / passes_u : 0u;
+  const size_t cap_blocks = per_block ? sample_buffer_cap() / per_block : nblocks;
   // 32-bit item indices. After the queue drains, every wave may still bump the counter
   // once per lane (each claim retires >= 1 lane): <= 8 blocks/CU x 4 waves x 64 x 64 on
   // 256 CUs = 2^25 past n_items, so keep 2^28 of headroom below 2^32.
   constexpr uint32_t kItemLimit = 0xFFFFFFFFu - (1u << 28);
-  if (kp.P && nb_pass > kItemLimit / kp.P) nb_pass = kItemLimit / kp.P;
-  if (nb_pass < 1) nb_pass = 1;
-  if (nb_pass > nblocks) nb_pass = nblocks;
-  const int passes = nblocks ? static_cast<int>((nblocks + nb_pass - 1) / nb_pass) : 0;
-  if (kp.P && nb_pass && per_block * nb_pass > c->cap_samples) {
+  uint32_t nb_max = static_cast<uint32_t>(passes_u > 1 ? cap_blocks / 2 : cap_blocks);
+  if (kp.P && nb_max > kItemLimit / kp.P) nb_max = kItemLimit / kp.P;
+  if (nb_max < 1) nb_max = 1;
+  if (nb_pass > nb_max) {
+    nb_pass = nb_max;
+    if (nblocks > nb_pass && nb_pass > static_cast<uint32_t>(cap_blocks / 2) && cap_blocks / 2 >= 1)
+      nb_pass = static_cast<uint32_t>(cap_blocks / 2);  // two slots must fit
+  }
+  const int passes = nb_pass ? static_cast<int>((nblocks + nb_pass - 1) / nb_pass) : 0;
+  const int slots = passes > 1 ? 2 : 1;
+  const size_t slot_bytes = per_block * nb_pass;
+  if (kp.P && nb_pass && slot_bytes * slots > c->cap_samples) {
     if (c->d_samples) HIPCHK(hipFree(c->d_samples));
     c->d_samples = nullptr;
     c->cap_samples = 0;
-    HIPCHK(hipMalloc(&c->d_samples, per_block * nb_pass));
-    c->cap_samples = per_block * nb_pass;
+    HIPCHK(hipMalloc(&c->d_samples, slot_bytes * slots));
+    c->cap_samples = slot_bytes * slots;
   }
   const size_t running_bytes = static_cast<size_t>(kp.P) * 3 * sizeof(float);
   if (passes > 1 && running_bytes > c->cap_running) {
@@ -1216,7 +1241,12 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
     HIPCHK(hipMalloc(&c->d_running, running_bytes));
     c->cap_running = running_bytes;
   }
-  while (c->ev_trace.size() < 2u * static_cast<size_t>(passes)) {
+  while (c->ev_sum.size() < static_cast<size_t>(passes > 0 ? passes : 1)) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->ev_sum.push_back(e);
+  }
+  while (c->ev_trace.size() < 2u * static_cast<size_t>(passes > 0 ? passes : 1)) {
     hipEvent_t e;
     HIPCHK(hipEventCreate(&e));
     c->ev_trace.push_back(e);
@@ -1229,8 +1259,6 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
   const size_t lds = n_att * 16 + n_rec * 64 + stack_bytes;
   KWork kw;
-  kw.queue = reinterpret_cast<uint32_t*>(c->d_cnt + 31);
-  kw.samples = c->d_samples;
   kw.counters = c->d_cnt;
   c->t0 = std::chrono::steady_clock::now();
   HIPCHK(hipMemsetAsync(c->d_cnt, 0, 32 * sizeof(unsigned long long), c->stream));
@@ -1242,29 +1270,43 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   }
 #endif
   HIPCHK(hipEventRecord(c->ev0, c->stream));
+  HIPCHK(hipEventRecord(c->ev_start, c->stream));
+  HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
+  HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_start, 0));
   const uint32_t sum_blocks = (kp.P + 255u) / 256u;
   int traced = 0;  // trace launches whose events were recorded
+  int summed = 0;
   for (int pass = 0; pass < passes || (pass == 0 && kp.P); ++pass) {
+    const int slot = pass % 2;
+    hipStream_t ts = slot ? c->stream2 : c->stream;
+    float* samples = c->d_samples ? c->d_samples + static_cast<size_t>(slot) * (slot_bytes / sizeof(float)) : nullptr;
     kp.b0 = static_cast<uint32_t>(pass) * nb_pass;
     kp.nb = pass < passes ? min(nb_pass, nblocks - kp.b0) : 0u;
     kp.n_items = kp.nb * kp.P;
     if (kp.n_items) {
+      if (pass >= 2) HIPCHK(hipStreamWaitEvent(ts, c->ev_sum[pass - 2], 0));  // the slot's last reader is done
+      kw.queue = reinterpret_cast<uint32_t*>(c->d_cnt + 31 - slot);
+      kw.samples = samples;
       // persistent grid: enough waves to fill every CU (extra blocks find the queue empty)
       const uint64_t want = (static_cast<uint64_t>(kp.n_items) + 255u) / 256u;
       const uint32_t blocks = static_cast<uint32_t>(want < 8ull * c->num_cus ? want : 8ull * c->num_cus);
-      HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), c->stream));
-      HIPCHK(hipEventRecord(c->ev_trace[2 * traced], c->stream));
-      launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, dim3(blocks), lds, c->stream, ks, kc, kp, kw);
+      HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), ts));
+      HIPCHK(hipEventRecord(c->ev_trace[2 * traced], ts));
+      launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, dim3(blocks), lds, ts, ks, kc, kp, kw);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(c->ev_trace[2 * traced + 1], c->stream));
+      HIPCHK(hipEventRecord(c->ev_trace[2 * traced + 1], ts));
+      HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_trace[2 * traced + 1], 0));
       ++traced;
     }
     const int first = pass == 0, last = pass + 1 >= passes;
-    hipLaunchKernelGGL(sum_kernel, dim3(sum_blocks ? sum_blocks : 1u), dim3(256), 0, c->stream, kp, c->d_samples,
+    hipLaunchKernelGGL(sum_kernel, dim3(sum_blocks ? sum_blocks : 1u), dim3(256), 0, c->stream_sum, kp, samples,
                        c->d_running, c->d_mean, c->d_u8, first, last);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_sum[pass], c->stream_sum));
+    summed = pass + 1;
     if (last) break;
   }
+  if (summed) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_sum[summed - 1], 0));
   c->passes = traced;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   c->last = *p;

@@ -487,3 +487,20 @@ def test_absorbed_paths_skip_unwind_only_when_exact(gpu, colors):
     omean, ou8, ocnt, _ = O.render(prims, O.camera_new(w, h), w, h, spp, depth, seed=5, threads=8)
     assert_parity(mean, u8, st, omean, ou8, ocnt)
     assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
+
+
+@pytest.mark.parametrize("pipe,buf_gb", [("1", None), ("2", None), ("3", None), ("5", None), ("2", "0.0002")])
+def test_pass_pipeline_never_changes_results(gpu, pipe, buf_gb, monkeypatch):
+    """Passes on alternating streams with a double-buffered sample buffer (and, with a
+    tiny FR_SAMPLE_BUFFER_GB, many passes reusing the two slots) give the same bits."""
+    w, h, spp = 64, 40, 70  # 5 blocks, the last partial
+    sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
+    monkeypatch.setenv("FR_PIPELINE", "1")
+    monkeypatch.delenv("FR_SAMPLE_BUFFER_GB", raising=False)
+    ref = gpu.render(sc, sc.camera, w, h, spp, 8)
+    monkeypatch.setenv("FR_PIPELINE", pipe)
+    if buf_gb:
+        monkeypatch.setenv("FR_SAMPLE_BUFFER_GB", buf_gb)
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, 8)
+    assert np.array_equal(mean.view(np.uint32), ref[0].view(np.uint32)) and np.array_equal(u8, ref[1])
+    assert (st["segments"], st["hits"]) == (ref[2]["segments"], ref[2]["hits"])
