@@ -46,7 +46,12 @@ def main():
     shas = {}
     for _ in range(a.reps):
         for lib in a.libs:
-            env = dict(os.environ, FORMA_RT_LIB=os.path.abspath(lib))
+            # "lib.so@NAME=VALUE,..." runs that library with extra environment settings
+            path, _, extra = lib.partition("@")
+            env = dict(os.environ, FORMA_RT_LIB=os.path.abspath(path))
+            for kv in filter(None, extra.split(",")):
+                k, _, v = kv.partition("=")
+                env[k] = v
             out = subprocess.run([sys.executable, "-c", CHILD, ROOT, a.scene, str(w), str(h), str(a.spp),
                                   str(a.depth), str(a.steps), str(a.shards)], env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
@@ -59,7 +64,7 @@ def main():
     for lib in a.libs:
         ms = sorted(res[lib])[len(res[lib]) // 2]
         samples = w * h * a.spp / a.shards
-        print(f"{os.path.basename(lib):32s} {ms:9.3f} ms  {samples / ms / 1e3:10.1f} Msamples/s  "
+        print(f"{os.path.basename(lib):40s} {ms:9.3f} ms  {samples / ms / 1e3:10.1f} Msamples/s  "
               f"{'same image' if shas[lib] == base else 'IMAGE DIFFERS ' + shas[lib]}")
 
 
