@@ -201,14 +201,17 @@ def main():
     segs = sum(s["segments"] for s in stats)
     hits = sum(s["hits"] for s in stats)
     kernel_ms = sum(s["kernel_ms"] for s in stats) / max(1, len(stats))
-    trace_ms = sum(s["trace_ms"] for s in stats) / max(1, len(stats))  # trace_kernel alone (one launch at C3)
+    trace_ms = sum(s["trace_ms"] for s in stats) / max(1, len(stats))  # trace_kernel launches of one frame
+    launches = max(1, stats[0]["trace_launches"])                       # sample-block passes
+    launch_ms = trace_ms / launches                                       # what rocprof's average reports
     kernel_ms_max = barrier.max(kernel_ms)
     total_segs = barrier.sum(segs)
 
     # roofline of the dominant kernel (trace_kernel), per launch on this rank
     pixels = len(shard_rows(HEIGHT, rank, world)) * WIDTH
-    bytes_launch = algorithmic_bytes(pixels, n_prims)
-    achieved = bytes_launch / (trace_ms * 1e-3) / 1e9
+    # a launch renders 1/launches of the frame's samples: its share of the frame's bytes
+    bytes_launch = algorithmic_bytes(pixels, n_prims) / launches
+    achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(PMC_FILE):
         try:
@@ -217,8 +220,8 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    flops_launch = algorithmic_flops(segs / len(stats), hits / len(stats), my_samples / len(stats), n_prims)
-    tflops = flops_launch / (trace_ms * 1e-3) / 1e12
+    flops_launch = algorithmic_flops(segs / len(stats), hits / len(stats), my_samples / len(stats), n_prims) / launches
+    tflops = flops_launch / (launch_ms * 1e-3) / 1e12
 
     checksum = None
     if a.verify:
@@ -249,10 +252,12 @@ def main():
         "segments_per_sample": round(total_segs / max(1.0, total_samples), 4),
         "kernel_ms": round(kernel_ms, 3),
         "trace_kernel_ms": round(trace_ms, 3),
+        "trace_launches": launches,
+        "trace_kernel_ms_per_launch": round(launch_ms, 3),
         "kernel_ms_max_rank": round(kernel_ms_max, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 8), "traffic": traffic,
-                     "kernel": "trace_kernel", "bytes_per_launch": bytes_launch},
+                     "kernel": "trace_kernel", "bytes_per_launch": round(bytes_launch)},
         "valu_roofline": {"bound": "valu", "achieved": round(tflops, 3), "peak": FP32_PEAK_TFLOPS,
                           "unit": "TFLOP/s", "frac": round(tflops / FP32_PEAK_TFLOPS, 5),
                           "flops_per_launch": int(flops_launch), "note": "algorithmic lower bound, DESIGN.md §5"},

@@ -79,7 +79,7 @@ static_assert(kBatch >= 1 && kBatch <= 64 && (kBatch & (kBatch - 1)) == 0, "kBat
 static_assert(sizeof(fr_prim) == 88, "fr_prim layout");
 static_assert(sizeof(fr_camera) == 104, "fr_camera layout");
 static_assert(sizeof(fr_params) == 40, "fr_params layout");
-static_assert(sizeof(fr_stats) == 56, "fr_stats layout");
+static_assert(sizeof(fr_stats) == 64, "fr_stats layout");
 
 struct DeviceCopy {
   int device = -1;
@@ -1203,10 +1203,12 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   const uint32_t nblocks = (p->spp + kBlockSamples - 1) / kBlockSamples;
   // Passes of nb_pass blocks each. With more than one pass the sample buffer holds two
   // pass slots (a pass traces into one while the previous pass's sum reads the other).
-  // FR_PIPELINE (default 2) asks for at least that many passes; the buffer budget
-  // (FR_SAMPLE_BUFFER_GB) may force more.
+  // FR_PIPELINE (default 1) asks for at least that many passes; the buffer budget
+  // (FR_SAMPLE_BUFFER_GB) may force more. Two pipelined passes measured 0.6 % faster
+  // on C3, but overlapping launches blur each launch's own HIP-event time (DESIGN.md
+  // §4.5a), so one pass is the default.
   const size_t per_block = static_cast<size_t>(kp.P) * kBlockSamples * 3 * sizeof(float);
-  uint32_t want_passes = 2;
+  uint32_t want_passes = 1;
   if (const char* e = getenv("FR_PIPELINE")) want_passes = static_cast<uint32_t>(atoi(e) > 0 ? atoi(e) : 1);
   uint32_t passes_u = nblocks ? (want_passes < nblocks ? want_passes : nblocks) : 0u;
   uint32_t nb_pass = passes_u ? (nblocks + passes_u - 1) / passes_u : 0u;
@@ -1376,6 +1378,8 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
       tms += t;
     }
     st->trace_ms = tms;
+    st->trace_launches = static_cast<uint32_t>(c->passes);
+    st->reserved = 0;
     st->total_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t0).count();
   }
@@ -1478,6 +1482,7 @@ int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* 
       stats->prim_tests += sts[g].prim_tests;
       if (sts[g].kernel_ms > stats->kernel_ms) stats->kernel_ms = sts[g].kernel_ms;
       if (sts[g].trace_ms > stats->trace_ms) stats->trace_ms = sts[g].trace_ms;
+      if (sts[g].trace_launches > stats->trace_launches) stats->trace_launches = sts[g].trace_launches;
     }
     stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }

@@ -67,7 +67,8 @@ class FrParams(C.Structure):
 
 class FrStats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("hits", C.c_uint64), ("samples", C.c_uint64), ("prim_tests", C.c_uint64),
-                ("kernel_ms", C.c_double), ("total_ms", C.c_double), ("trace_ms", C.c_double)]
+                ("kernel_ms", C.c_double), ("total_ms", C.c_double), ("trace_ms", C.c_double),
+                ("trace_launches", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

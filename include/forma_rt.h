@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define FR_ABI_VERSION 1
+#define FR_ABI_VERSION 2 /* 2: fr_stats.trace_launches; FR_TRIANGLE; post effects; FR_FLAG_MT_BANDS */
 
 /* error codes */
 #define FR_OK 0
@@ -139,7 +139,9 @@ typedef struct fr_stats {
   uint64_t prim_tests; /* segments * n_prims */
   double kernel_ms;    /* HIP-event time of the whole render on its stream (all kernels) */
   double total_ms;     /* host wall time of the call */
-  double trace_ms;     /* HIP-event time of the trace kernel(s) alone */
+  double trace_ms;     /* HIP-event time of the trace kernel(s) alone, summed over launches */
+  uint32_t trace_launches; /* trace kernel launches of the render (sample-block passes) */
+  uint32_t reserved;
 } fr_stats;
 
 typedef struct fr_scene fr_scene; /* opaque: host primitive list + per-device copies */
