@@ -504,3 +504,43 @@ def test_pass_pipeline_never_changes_results(gpu, pipe, buf_gb, monkeypatch):
     mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, 8)
     assert np.array_equal(mean.view(np.uint32), ref[0].view(np.uint32)) and np.array_equal(u8, ref[1])
     assert (st["segments"], st["hits"]) == (ref[2]["segments"], ref[2]["hits"])
+
+
+@pytest.mark.slow
+def test_c4_shard_on_row_subset(gpu):
+    """C4 (scene_08 3840x2160, 1024 spp, 8 bounces) as one of 8 ranks renders it: shard 0
+    of 8 (8-row strips 0, 8, 16, ...), checked on a subset of that shard's rows. The
+    render runs in passes (the sample buffer holds 21 of its 64 blocks)."""
+    w, h, spp, depth = 3840, 2160, 1024, 8
+    sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth, shard_index=0, shard_count=8)
+    mine = [y for y in range(h) if (y // 8) % 8 == 0]
+    assert st["samples"] == len(mine) * w * spp
+    prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path("scene_08")).read())
+    cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
+    omean, ou8, _, n = O.render(prims, cam, w, h, spp, depth, shard_index=0, shard_count=8, row_step=97,
+                                threads=16)
+    rows = mine[::97]
+    assert n == len(rows) and len(rows) >= 3
+    assert_parity(mean, u8, st, omean, ou8, None, rows=rows)
+
+
+@pytest.mark.slow
+def test_c5_generator_scene_on_row_subset(gpu):
+    """C5 (10k spheres, 1920x1080, 512 spp, 8 bounces, BVH path) on two rows the oracle's
+    brute-force list loop renders."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_scene", os.path.join(ROOT, "tools", "gen_scene.py"))
+    gs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gs)
+    text = gs.dumps(gs.generator_scene(10000, "sphere"))
+    w, h, spp, depth = 1920, 1080, 512, 8
+    sc = gpu.Scene.from_json(text, w, h)
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
+    prims, (frm, at, vup, fov) = S.load_json(text)
+    cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
+    omean, ou8, _, n = O.render(prims, cam, w, h, spp, depth, row_step=539, threads=16)
+    rows = list(range(0, h, 539))
+    assert n == len(rows)
+    assert_parity(mean, u8, st, omean, ou8, None, rows=rows)
+    assert np.isfinite(mean).all()
