@@ -302,22 +302,28 @@ template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT>
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) FR_OCC_ATTR void trace_kernel(
     KScene sc, KCam cam, KParams kp, KWork kw) {
-  // LDS: [n_att x (attenuation rgb, scatter class bits)][n_rec x 64-B record]
-  //      [stack: MAXD ? MAXD x kBlock u16 : max_depth x kBlock u32]
+  // LDS: [n_att + 1 x (attenuation rgb, scatter class bits)][n_rec x 64-B record]
+  //      [stack: MAXD ? kBlock x MAXD u16 (lane-major) : max_depth x kBlock u32]
+  // Entry n of the attenuations is (1, 1, 1): the depth-8 stack's empty levels hold n.
   // Staging the winner's data keeps per-lane global gathers off the shading path.
   extern __shared__ uint32_t lds[];
   __shared__ uint32_t wq_next[kBlock / 64], wq_end[kBlock / 64];  // per-wave item batch
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
+  const uint32_t n_att_st = n_att ? n_att + 1u : 0u;  // with the unit entry
   const uint32_t n_rec = sc.n <= kRecLds ? sc.n : 0u;
   float4* att_lds = reinterpret_cast<float4*>(lds);
-  float4* rec_lds = att_lds + n_att;
+  float4* rec_lds = att_lds + n_att_st;
   uint32_t* stack = reinterpret_cast<uint32_t*>(rec_lds + 4u * n_rec);
   uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u, wave = tid >> 6;
-  for (uint32_t i = tid; i < n_att; i += kBlock) {
+  static_assert(MAXD == 0 || MAXD == 8, "the u16 stack is one 16-B row per lane");
+  uint4* hrow = reinterpret_cast<uint4*>(stack) + tid;  // this lane's MAXD = 8 levels
+  const uint32_t unit2 = sc.n | (sc.n << 16);            // two empty levels
+  if (MAXD > 0) *hrow = make_uint4(unit2, unit2, unit2, unit2);
+  for (uint32_t i = tid; i < n_att_st; i += kBlock) {
     const float4 a = sc.att[i];
-    att_lds[i] = make_float4(a.x, a.y, a.z, __uint_as_float(sc.cls[i]));
+    att_lds[i] = make_float4(a.x, a.y, a.z, __uint_as_float(i < n_att ? sc.cls[i] : 0u));
   }
   for (uint32_t i = tid; i < 4u * n_rec; i += kBlock) rec_lds[i] = sc.rec[i];
   if (lane == 0) {
@@ -344,7 +350,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // stack push at level `depth` of the scatter winner
   auto push = [&](uint32_t pi) {
     if (MAXD > 0)
-      hstack[depth * kBlock + tid] = static_cast<uint16_t>(pi);
+      hstack[tid * MAXD + depth] = static_cast<uint16_t>(pi);
     else
       stack[depth * kBlock + tid] = pi;
   };
@@ -671,33 +677,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       DIAG_WAVE(DG_END_W);
       DIAG_LANE(DG_END_L);
       V3 col = term;
-      // An absorbed path (terminal colour +0) stays +0 through any chain of finite,
-      // non-negative attenuations: skip its unwind (sc.att_nonneg is the host's check).
-      const bool zero_term = (__float_as_uint(term.x) | __float_as_uint(term.y) | __float_as_uint(term.z)) == 0u;
-      const int udepth = sc.att_nonneg && zero_term ? 0 : static_cast<int>(depth);
-      // n_att is wave-uniform: one unwind per attenuation source keeps LDS reads as
-      // ds_read (a merged pointer would become flat loads)
-      if (MAXD > 0 && n_att) {
+      if (MAXD > 0) {
+        // One read brings the lane's 8 levels; empty ones point at the unit entry
+        // (x * 1.0f == x), so the product a0*(a1*(...*term)) needs no per-level branch
+        // and its reads do not wait on each other.
+        const uint4 w = *hrow;
+        *hrow = make_uint4(unit2, unit2, unit2, unit2);  // the next sample starts empty
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+        if (n_att) {
 #pragma unroll
-        for (int j = MAXD - 1; j >= 0; --j) {
-          if (j < udepth) {
+          for (int j = MAXD - 1; j >= 0; --j) {
             DIAG_WAVE(DG_UNW_W);
-            DIAG_LANE(DG_UNW_L);
-            const uint32_t pi = hstack[j * kBlock + tid];
+            const uint32_t pi = (ws[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
             col = mul(xyz(att_lds[pi]), col);
           }
-        }
-      } else if (MAXD > 0) {
+        } else {
+          // global attenuations: only the levels in use
 #pragma unroll
-        for (int j = MAXD - 1; j >= 0; --j)
-          if (j < udepth) col = mul(xyz(sc.att[hstack[j * kBlock + tid]]), col);
-      } else if (n_att) {
-        for (int j = udepth - 1; j >= 0; --j) {
-          const uint32_t pi = stack[j * kBlock + tid];
-          col = mul(xyz(att_lds[pi]), col);
+          for (int j = MAXD - 1; j >= 0; --j)
+            if (j < static_cast<int>(depth)) col = mul(xyz(sc.att[(ws[j >> 1] >> (16 * (j & 1))) & 0xFFFFu]), col);
         }
       } else {
-        for (int j = udepth - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
+        // An absorbed path (terminal colour +0) stays +0 through any chain of finite,
+        // non-negative attenuations: skip its unwind (sc.att_nonneg is the host's check).
+        const bool zero_term = (__float_as_uint(term.x) | __float_as_uint(term.y) | __float_as_uint(term.z)) == 0u;
+        const int udepth = sc.att_nonneg && zero_term ? 0 : static_cast<int>(depth);
+        if (n_att) {
+          for (int j = udepth - 1; j >= 0; --j) {
+            const uint32_t pi = stack[j * kBlock + tid];
+            col = mul(xyz(att_lds[pi]), col);
+          }
+        } else {
+          for (int j = udepth - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
+        }
       }
       out[0] = col.x;
       out[1] = col.y;
@@ -883,7 +895,7 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   c->off_cls = off;
   off = align_up(off + m * 4, 256);
   c->off_att = off;
-  off = align_up(off + m * 16, 256);
+  off = align_up(off + (static_cast<size_t>(n) + 1) * 16, 256);  // + the unit entry
   c->off_rec = off;
   off = align_up(off + m * 64, 256);
   c->off_bvh = off;
@@ -901,7 +913,6 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   if (!bvh_segs.empty()) memcpy(&host[c->off_segs], bvh_segs.data(), bvh_segs.size() * sizeof(BvhSegment));
   c->bvh_n = static_cast<uint32_t>(bvh_nodes.size());
   c->n_segs = static_cast<uint32_t>(bvh_segs.size());
-  c->att_nonneg = nonneg;
   for (uint32_t i = 0; i < n; ++i) {
     const fr_prim& p = s->prims[i];
     uint32_t kind = p.kind;
@@ -948,6 +959,12 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
       if (!(a >= 0.0f) || std::signbit(a) || !std::isfinite(a)) nonneg = false;
     memcpy(&g[3].w, &kind, 4);  // kind bits in g3.w
     memcpy(&host[c->off_rec + 64 * i], g, 64);
+  }
+  c->att_nonneg = nonneg;
+  {
+    // entry n: the unit attenuation the depth-8 stack's empty levels point at
+    const float4 one = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    memcpy(&host[c->off_att + 16 * n], &one, 16);
   }
   if (n == 0) {
     const uint32_t stub = FR_STUB;
@@ -1259,7 +1276,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
                                          : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
                                                sizeof(uint32_t);
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
-  const size_t lds = n_att * 16 + n_rec * 64 + stack_bytes;
+  const size_t lds = (n_att ? n_att + 1 : 0) * 16 + n_rec * 64 + stack_bytes;
   KWork kw;
   kw.counters = c->d_cnt;
   c->t0 = std::chrono::steady_clock::now();

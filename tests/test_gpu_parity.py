@@ -544,3 +544,21 @@ def test_c5_generator_scene_on_row_subset(gpu):
     assert n == len(rows)
     assert_parity(mean, u8, st, omean, ou8, None, rows=rows)
     assert np.isfinite(mean).all()
+
+
+@pytest.mark.parametrize("depth", [8, 12])
+def test_absorbed_path_through_infinite_attenuation_is_nan(gpu, depth):
+    """A fuzzy metal whose colour has an infinite component: an absorbed path (terminal
+    +0) behind it is 0 * inf = NaN in the recursion (tracer.rs:206-207), so no unwind
+    may be skipped there. depth 8 runs the u16-stack kernel, 12 the u32 one."""
+    w, h, spp = 24, 16, 4
+    prims = [S.sphere([0.0, 0.0, -2.0], 0.9, S.METAL, [np.inf, 0.5, 0.5], 1.0),
+             S.sphere([0.0, -100.9, -2.0], 100.0, S.LAMBERTIAN, [0.5, 0.5, 0.5], 0.0)]
+    sc = gpu.Scene.from_prims(prims)
+    cam = gpu.camera_new(w, h)
+    mean, u8, st = gpu.render(sc, cam, w, h, spp, depth, seed=77)
+    omean, ou8, ocnt, _ = O.render(prims, O.camera_new(w, h), w, h, spp, depth, seed=77, threads=8)
+    assert np.isnan(omean).any(), "fixture must absorb some path behind the metal"
+    assert _same_bits(mean, omean)
+    assert np.array_equal(u8, ou8)
+    assert (st["segments"], st["hits"]) == (ocnt["segments"], ocnt["hits"])
