@@ -157,6 +157,13 @@ struct KCam {
   float px, py, pz, lx, ly, lz, hx, hy, hz, vx, vy, vz, ux, uy, uz, bx, by, bz, lens;
 };
 
+struct KArgs {
+  KScene sc;
+  KCam cam;
+  KParams kp;
+  KWork kw;
+};
+
 // Effective scatter class after each shape's fallback chain
 // (sphere.rs:56-69: 0/1/2/3 else lambertian; plane.rs:48-59: 1 metal else lambertian).
 static uint32_t scatter_class(const fr_prim& p) {
@@ -301,7 +308,12 @@ template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT>
 #define FR_OCC_ATTR
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) FR_OCC_ATTR void trace_kernel(
-    KScene sc, KCam cam, KParams kp, KWork kw) {
+    KArgs args) {
+  // one by-value struct: the kernarg segment holds it at offset 0 (the camera is read
+  // back from there in the lens step)
+  const KScene& sc = args.sc;
+  const KParams& kp = args.kp;
+  const KWork& kw = args.kw;
   // LDS: [n_att + 1 x (attenuation rgb, scatter class bits)][n_rec x 64-B record]
   //      [stack: MAXD ? kBlock x MAXD u16 (lane-major) : max_depth x kBlock u32]
   // Entry n of the attenuations is (1, 1, 1): the depth-8 stack's empty levels hold n.
@@ -458,7 +470,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       if (acc) {
         if (!sph) {
           // Camera::get_ray (camera.rs:62-72)
-          const KCam& cm = cam;
+#if !defined(FR_CAM_RESIDENT) && defined(__HIP_DEVICE_COMPILE__)
+          // scalar loads of the camera from the kernarg segment, here, rather than 19
+          // SGPRs held (and spilled) across the loop: the pointer is opaque to the
+          // compiler, so the loads stay in this step
+          typedef __attribute__((address_space(4))) const KArgs cargs;
+          cargs* ap = (cargs*)(__builtin_amdgcn_kernarg_segment_ptr());
+          asm volatile("" : "+s"(ap));
+          const KCam cm = ap->cam;
+#else
+          const KCam& cm = args.cam;
+#endif
           const V3 cpos{cm.px, cm.py, cm.pz}, cllc{cm.lx, cm.ly, cm.lz}, chor{cm.hx, cm.hy, cm.hz};
           const V3 cver{cm.vx, cm.vy, cm.vz}, cu{cm.ux, cm.uy, cm.uz}, cv{cm.bx, cm.by, cm.bz};
           const V3 rd = scl(cm.lens, V3{px, py, 0.0f});
@@ -565,6 +587,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           }
         }
       }
+#ifdef FR_HIT_UNROLL
+#pragma unroll FR_HIT_UNROLL
+#endif
       for (uint32_t ii = 0; ii < (BVH ? 0u : sc.n); ++ii) {
         // the index is wave-uniform; say so, or the compiler may fall back to vector loads
         const uint32_t i = __builtin_amdgcn_readfirstlane(ii);
@@ -1035,10 +1060,10 @@ template <int KS, bool HP, bool BV, bool MT = false>
 static void launch_depth(bool small_depth, dim3 g, size_t lds, hipStream_t st, const KScene& ks, const KCam& kc,
                          const KParams& kp, const KWork& kw) {
   if (small_depth)
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV, MT>), g, dim3(kBlock), lds, st, ks, kc, kp,
-                       kw);
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV, MT>), g, dim3(kBlock), lds, st,
+                       KArgs{ks, kc, kp, kw});
   else
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0, BV, MT>), g, dim3(kBlock), lds, st, ks, kc, kp, kw);
+    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0, BV, MT>), g, dim3(kBlock), lds, st, KArgs{ks, kc, kp, kw});
 }
 
 // BVH kernels walk the list's segments (bvh.h); scenes with planes use the general
