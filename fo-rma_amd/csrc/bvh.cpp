@@ -211,7 +211,7 @@ bool build_bvh(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end, 
 }
 
 bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& segs, std::vector<BvhNode>& nodes,
-                    std::vector<uint32_t>& order) {
+                    std::vector<uint32_t>& order, bool force) {
   segs.clear();
   nodes.clear();
   order.clear();
@@ -221,7 +221,8 @@ bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& 
   float cost = 0.0f;
   for (const fr_prim& p : prims)
     cost += p.kind == FR_TRIANGLE ? 2.5f : p.kind == FR_OBB ? 2.0f : (p.kind == FR_STUB ? 0.0f : 1.0f);
-  if (n < kBvhMinPrims || cost < kBvhMinCost || planes > kBvhMaxPlanes) return false;
+  if (planes > kBvhMaxPlanes || n == 0) return false;
+  if (!force && (n < kBvhMinPrims || cost < kBvhMinCost)) return false;
   const float pad = 1e-4f * scene_abs_max(prims) + 1e-4f;
   uint32_t i = 0;
   while (i < n) {

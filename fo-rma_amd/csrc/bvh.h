@@ -53,9 +53,10 @@ static_assert(sizeof(BvhSegment) == 16, "BvhSegment is one uint4");
 
 constexpr uint32_t kBvhMaxPlanes = 32;  // more planes: the in-order loop
 
-// Segments and trees for a scene; false if the scene is too small or has too many planes.
+// Segments and trees for a scene; false if the scene is too small or has too many planes
+// (`force` drops the size and cost thresholds, for A/B runs).
 bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& segs, std::vector<BvhNode>& nodes,
-                    std::vector<uint32_t>& order);
+                    std::vector<uint32_t>& order, bool force = false);
 
 }  // namespace fr
 

@@ -319,7 +319,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // Entry n of the attenuations is (1, 1, 1): the depth-8 stack's empty levels hold n.
   // Staging the winner's data keeps per-lane global gathers off the shading path.
   extern __shared__ uint32_t lds[];
-  __shared__ uint32_t wq_next[kBlock / 64], wq_end[kBlock / 64];  // per-wave item batch
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
   const uint32_t n_att_st = n_att ? n_att + 1u : 0u;  // with the unit entry
   const uint32_t n_rec = sc.n <= kRecLds ? sc.n : 0u;
@@ -328,7 +327,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   uint32_t* stack = reinterpret_cast<uint32_t*>(rec_lds + 4u * n_rec);
   uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
   const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63u, wave = tid >> 6;
+  const uint32_t lane = tid & 63u;
   static_assert(MAXD == 0 || MAXD == 8, "the u16 stack is one 16-B row per lane");
   uint4* hrow = reinterpret_cast<uint4*>(stack) + tid;  // this lane's MAXD = 8 levels
   const uint32_t unit2 = sc.n | (sc.n << 16);            // two empty levels
@@ -338,14 +337,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     att_lds[i] = make_float4(a.x, a.y, a.z, __uint_as_float(i < n_att ? sc.cls[i] : 0u));
   }
   for (uint32_t i = tid; i < 4u * n_rec; i += kBlock) rec_lds[i] = sc.rec[i];
-  if (lane == 0) {
-    wq_next[wave] = 0;
-    wq_end[wave] = 0;
-  }
 #ifdef FR_DIAG
   __shared__ uint32_t dg[DG_N];
   if (tid < DG_N) dg[tid] = 0;
-  const uint32_t gw = blockIdx.x * (kBlock / 64u) + wave;
+  const uint32_t gw = blockIdx.x * (kBlock / 64u) + (tid >> 6);
   if (lane == 0 && gw < 65536) {
     g_fr_wave_times[2 * gw] = __builtin_amdgcn_s_memrealtime();
     g_fr_wave_drain[gw] = ~0ull;
@@ -384,57 +379,61 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   uint64_t pf_acc[PF_N] = {0, 0, 0, 0, 0};
   uint64_t pf_t = __builtin_amdgcn_s_memtime();
 #endif
+  // the wave's claimed item batch [q_next, q_end): wave-uniform, updated only under
+  // the uniform branch below, so it lives in scalar registers
+  uint32_t q_next = 0, q_end = 0;
   while (active) {
     DIAG_WAVE(DG_ITER);
-    if (need_item) {
-      // 0. claim a work item: the free lanes take consecutive items of the wave's
-      // batch; when it runs out, the first free lane claims the next 64 globally.
+    const unsigned long long m = __ballot(need_item);
+    if (m) {
+      // 0. claim work items: the free lanes take consecutive items of the wave's batch;
+      // when it runs out, the first free lane claims the next kBatch-multiple globally.
       // (Prefetching the next item in batched refill passes measured slower.)
-      const unsigned long long m = __ballot(1);
       const uint32_t n = static_cast<uint32_t>(__popcll(m));
       const uint32_t r = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-      const uint32_t next = wq_next[wave], end = wq_end[wave];
-      const uint32_t avail = end - next;
+      const uint32_t next = __builtin_amdgcn_readfirstlane(q_next);
+      const uint32_t avail = __builtin_amdgcn_readfirstlane(q_end) - next;
       uint32_t base = 0;
       // the lanes past the wave's batch need `want` items: reserve whole kBatch steps
       const uint32_t grab = n > avail ? (n - avail + kBatch - 1u) & ~(kBatch - 1u) : 0u;
+      const int first = __ffsll(static_cast<long long>(m)) - 1;
       if (grab) {
-        if (r == 0) base = atomicAdd(kw.queue, grab);
-        base = __builtin_amdgcn_readfirstlane(base);
+        if (static_cast<int>(lane) == first) base = atomicAdd(kw.queue, grab);
+        base = __builtin_amdgcn_readlane(base, first);
+        q_end = base + grab;
       }
+      q_next = grab ? base + (n - avail) : next + n;
       const uint32_t item = r < avail ? next + r : base + (r - avail);
-      if (r == 0) {
-        wq_next[wave] = grab ? base + (n - avail) : next + n;
-        if (grab) wq_end[wave] = base + grab;
-      }
-      if (item >= kp.n_items) {
+      if (need_item && item >= kp.n_items) {
 #ifdef FR_DIAG
         if (gw < 65536) atomicMin(&g_fr_wave_drain[gw], static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
 #endif
         active = false;  // queue drained
         continue;
       }
-      uint32_t b, x, y;
-      bool ok = item_xy(kp, item, b, q, x, y);
-      uint32_t yrow = kp.H - y;  // tracer.rs:171-172: v = ((H - y) + r) / H
-      if (MT) {
-        // render_mt (tracer.rs:86-103): band k from the top is thread t_id = 3 - k;
-        // v = ((t_height - y_band) + r) / H + t_id * 0.25; rows past 4 * t_height unused
-        const uint32_t k = kp.band_h ? y / kp.band_h : 4u;
-        ok = ok && k < 4u;
-        yrow = kp.band_h - (y - k * kp.band_h);
-        vofs = static_cast<float>(3u - k) * 0.25f;
-      }
-      if (ok) {
-        rng = rng_seed(kp.seed, y * kp.W + x, b);  // this block's stream
-        s = b * kBlockSamples;
-        out = kw.samples + 3 * (static_cast<size_t>(s - s_pass) * kp.P + q);
-        s_end = min(s + kBlockSamples, kp.spp);
-        fx = static_cast<float>(x);
-        fy = static_cast<float>(yrow);
-        need_jit = true;
-        need_item = false;
+      if (need_item) {
+        uint32_t b, x, y;
+        bool ok = item_xy(kp, item, b, q, x, y);
+        uint32_t yrow = kp.H - y;  // tracer.rs:171-172: v = ((H - y) + r) / H
+        if (MT) {
+          // render_mt (tracer.rs:86-103): band k from the top is thread t_id = 3 - k;
+          // v = ((t_height - y_band) + r) / H + t_id * 0.25; rows past 4 * t_height unused
+          const uint32_t k = kp.band_h ? y / kp.band_h : 4u;
+          ok = ok && k < 4u;
+          yrow = kp.band_h - (y - k * kp.band_h);
+          vofs = static_cast<float>(3u - k) * 0.25f;
+        }
+        if (ok) {
+          rng = rng_seed(kp.seed, y * kp.W + x, b);  // this block's stream
+          s = b * kBlockSamples;
+          out = kw.samples + 3 * (static_cast<size_t>(s - s_pass) * kp.P + q);
+          s_end = min(s + kBlockSamples, kp.spp);
+          fx = static_cast<float>(x);
+          fy = static_cast<float>(yrow);
+          need_jit = true;
+          need_item = false;
+        }
       }
     }
     if (need_jit) {
@@ -909,7 +908,10 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   std::vector<BvhSegment> bvh_segs;
   std::vector<BvhNode> bvh_nodes;
   std::vector<uint32_t> bvh_order;
-  if (!build_segments(s->prims, bvh_segs, bvh_nodes, bvh_order)) {
+  // FR_BVH=1 builds the BVH below the size/cost thresholds (A/B runs), FR_BVH=0 never uses it
+  const char* bvh_env = getenv("FR_BVH");
+  const bool force_bvh = bvh_env && strcmp(bvh_env, "1") == 0;
+  if (!build_segments(s->prims, bvh_segs, bvh_nodes, bvh_order, force_bvh)) {
     bvh_segs.clear();
     bvh_nodes.clear();
     bvh_order.clear();
