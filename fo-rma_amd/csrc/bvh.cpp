@@ -1,5 +1,6 @@
-// Host BVH build: binned SAH (12 bins on the centroid extent of the longest axis),
-// leaves of at most kBvhLeafMax primitives, emitted depth-first with escape links.
+// Host BVH build: binned SAH (12 bins on the centroid extent of the longest axis) with
+// leaves of at most kBvhLeafMax primitives, object-median splits where the depth cap
+// (kBvhStack) would otherwise be at risk, nodes holding both children's boxes.
 #include "bvh.h"
 
 #include <math.h>
@@ -75,47 +76,83 @@ struct Item {
   uint32_t index;
 };
 
+// internal levels a balanced split of n items needs: ceil(log2(ceil(n / leaf_max)))
+uint32_t balanced_levels(uint32_t n, uint32_t leaf_max) {
+  uint32_t leaves = (n + leaf_max - 1) / leaf_max, l = 0;
+  while ((1u << l) < leaves) ++l;
+  return l;
+}
+
 struct Builder {
   std::vector<Item>& items;
   std::vector<BvhNode>& nodes;
   float pad;
+  uint32_t leaf_max;
+  uint32_t slot_base;  // leaf slots are absolute positions in the shared order array
 
-  uint32_t order_base = 0;  // leaf indices are absolute positions in the shared order array
-
-  // Emits the subtree over items[begin, end) at nodes.size(); returns its node index.
-  uint32_t build(uint32_t begin, uint32_t end) {
-    const uint32_t at = static_cast<uint32_t>(nodes.size());
-    nodes.push_back(BvhNode{});
-    Box3 box, cbox;
+  Box3 bounds(uint32_t begin, uint32_t end, Box3* cbox) const {
+    Box3 box;
     for (uint32_t i = begin; i < end; ++i) {
       box.grow(items[i].box);
-      cbox.grow(items[i].c);
+      if (cbox) cbox->grow(items[i].c);
     }
-    for (int k = 0; k < 3; ++k) {  // conservative padding
-      nodes[at].lo[k] = box.lo[k] - pad;
-      nodes[at].hi[k] = box.hi[k] + pad;
-    }
+    return box;
+  }
+
+  // Reference to the subtree over items[begin, end) at depth `depth`.
+  uint32_t build(uint32_t begin, uint32_t end, uint32_t depth) {
     const uint32_t n = end - begin;
+    if (n <= leaf_max) return bvh_leaf_ref(slot_base + begin, n);
+    Box3 cbox;
+    const Box3 box = bounds(begin, end, &cbox);
+    // SAH while the subtree can still be finished below the cap by balanced splits
+    // (a median split at depth d with d + levels(n) = kBvhStack leaves the deepest
+    // internal node at kBvhStack - 1)
     uint32_t mid = begin;
-    if (n > kBvhLeafMax) mid = split(begin, end, box, cbox);
-    if (mid == begin || mid == end) {  // leaf
-      if (n > kBvhLeafMax) {           // no useful split (coincident centroids): halve by index
-        mid = begin + n / 2;
-      } else {
-        nodes[at].leaf = (n << 24) | (order_base + begin);
-        nodes[at].escape = static_cast<uint32_t>(nodes.size());
-        return at;
-      }
+    if (depth + balanced_levels(n, leaf_max) < kBvhStack) mid = sah_split(begin, end, box, cbox);
+    if (mid == begin || mid == end) mid = median_split(begin, end, cbox);
+    const uint32_t at = static_cast<uint32_t>(nodes.size());
+    nodes.push_back(BvhNode{});
+    const Box3 l = bounds(begin, mid, nullptr), r = bounds(mid, end, nullptr);
+    const uint32_t rl = build(begin, mid, depth + 1);
+    const uint32_t rr = build(mid, end, depth + 1);
+    BvhNode& nd = nodes[at];
+    // conservative padding
+    for (int k = 0; k < 3; ++k) {
+      nd.a[k] = l.lo[k] - pad;
+      nd.b[k] = l.hi[k] + pad;
     }
-    build(begin, mid);
-    build(mid, end);
-    nodes[at].leaf = 0;
-    nodes[at].escape = static_cast<uint32_t>(nodes.size());
+    nd.a[3] = r.lo[0] - pad;
+    nd.b[3] = r.hi[0] + pad;
+    nd.c[0] = r.lo[1] - pad;
+    nd.c[1] = r.lo[2] - pad;
+    nd.c[2] = r.hi[1] + pad;
+    nd.c[3] = r.hi[2] + pad;
+    nd.ref[0] = rl;
+    nd.ref[1] = rr;
     return at;
   }
 
-  // Binned SAH split; returns the partition point, or begin if a leaf is cheaper.
-  uint32_t split(uint32_t begin, uint32_t end, const Box3& box, const Box3& cbox) {
+  // Object median on the longest centroid axis; halves by index when the centroids
+  // coincide.
+  uint32_t median_split(uint32_t begin, uint32_t end, const Box3& cbox) {
+    int axis = 0;
+    float ext = -1.0f;
+    for (int k = 0; k < 3; ++k)
+      if (cbox.hi[k] - cbox.lo[k] > ext) {
+        ext = cbox.hi[k] - cbox.lo[k];
+        axis = k;
+      }
+    const uint32_t mid = begin + (end - begin) / 2;
+    if (ext > 0.0f)
+      std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end,
+                       [&](const Item& x, const Item& y) { return x.c[axis] < y.c[axis]; });
+    return mid;
+  }
+
+  // Binned SAH split; returns the partition point, or begin if none separates.
+  uint32_t sah_split(uint32_t begin, uint32_t end, const Box3& box, const Box3& cbox) {
+    (void)box;
     int axis = 0;
     float ext = -1.0f;
     for (int k = 0; k < 3; ++k)
@@ -159,10 +196,7 @@ struct Builder {
         best_b = b;
       }
     }
-    const uint32_t n = end - begin;
     if (best_b < 0) return begin;
-    // leaf cost n * area against 1 traversal + the split's cost
-    if (n <= kBvhLeafMax && best >= box.area() * n) return begin;
     auto it = std::partition(items.begin() + begin, items.begin() + end,
                              [&](const Item& x) { return bin_of(x) < best_b; });
     return static_cast<uint32_t>(it - items.begin());
@@ -179,8 +213,10 @@ float scene_abs_max(const std::vector<fr_prim>& prims) {
   return m;
 }
 
+// Builds the tree over the boundable primitives of prims[begin, end); `root` is its
+// reference (kBvhEnd when none is boundable). False if it cannot be encoded.
 bool build_range(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end, float pad,
-                 std::vector<BvhNode>& nodes, std::vector<uint32_t>& order) {
+                 std::vector<BvhNode>& nodes, std::vector<uint32_t>& order, uint32_t& root) {
   std::vector<Item> items;
   items.reserve(end - begin);
   for (uint32_t i = begin; i < end; ++i) {
@@ -190,25 +226,28 @@ bool build_range(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end
     it.index = i;
     items.push_back(it);
   }
-  if (items.empty()) return false;
-  // Leaf indices must fit the node's 24-bit field.
-  if (order.size() + items.size() >= (1u << 24)) return false;
-  Builder b{items, nodes, pad};
-  b.order_base = static_cast<uint32_t>(order.size());
-  b.build(0, static_cast<uint32_t>(items.size()));
+  root = kBvhEnd;
+  if (items.empty()) return true;
+  const uint32_t n = static_cast<uint32_t>(items.size());
+  // leaves of kBvhLeafMax, larger only when the balanced depth would not fit the stack
+  uint32_t leaf_max = kBvhLeafMax;
+  while (balanced_levels(n, leaf_max) >= kBvhStack && leaf_max < kBvhLeafCountMax) leaf_max *= 2;
+  if (balanced_levels(n, leaf_max) >= kBvhStack) return false;
+  if (order.size() + n + kBvhLeafCountMax >= (1u << kBvhSlotBits)) return false;
+  if (nodes.size() + n >= kBvhLeaf) return false;
+  Builder b{items, nodes, pad, leaf_max, static_cast<uint32_t>(order.size())};
+  root = b.build(0, n, 0);
   for (const Item& it : items) order.push_back(it.index);
   return true;
 }
 
-}  // namespace
-
-bool build_bvh(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end, std::vector<BvhNode>& nodes,
-               std::vector<uint32_t>& order) {
-  // The cull must never reject a primitive whose own test accepts a hit: pad every box
-  // by a margin far above the f32 error of a root or a slab distance at scene scale.
-  const float pad = 1e-4f * scene_abs_max(prims) + 1e-4f;
-  return build_range(prims, begin, end, pad, nodes, order);
+uint32_t depth_of(const std::vector<BvhNode>& nodes, uint32_t ref, uint32_t depth) {
+  if (ref >= kBvhLeaf) return 0;
+  const BvhNode& nd = nodes[ref];
+  return std::max({depth, depth_of(nodes, nd.ref[0], depth + 1), depth_of(nodes, nd.ref[1], depth + 1)});
 }
+
+}  // namespace
 
 bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& segs, std::vector<BvhNode>& nodes,
                     std::vector<uint32_t>& order, bool force) {
@@ -223,23 +262,31 @@ bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& 
     cost += p.kind == FR_TRIANGLE ? 2.5f : p.kind == FR_OBB ? 2.0f : (p.kind == FR_STUB ? 0.0f : 1.0f);
   if (planes > kBvhMaxPlanes || n == 0) return false;
   if (!force && (n < kBvhMinPrims || cost < kBvhMinCost)) return false;
+  // The cull must never reject a primitive whose own test accepts a hit: pad every box
+  // by a margin far above the f32 error of a root or a slab distance at scene scale.
   const float pad = 1e-4f * scene_abs_max(prims) + 1e-4f;
   uint32_t i = 0;
   while (i < n) {
     if (prims[i].kind == FR_PLANE) {
-      segs.push_back(BvhSegment{1u, 0u, 0u, i});
+      segs.push_back(BvhSegment{1u, kBvhEnd, 0u, i});
       ++i;
       continue;
     }
     uint32_t j = i;
     while (j < n && prims[j].kind != FR_PLANE) ++j;
-    const uint32_t first = static_cast<uint32_t>(nodes.size());
-    if (!build_range(prims, i, j, pad, nodes, order) && nodes.size() != first) return false;
-    const uint32_t last = static_cast<uint32_t>(nodes.size());
-    if (last > first) segs.push_back(BvhSegment{0u, first, last, 0u});
+    uint32_t root = kBvhEnd;
+    if (!build_range(prims, i, j, pad, nodes, order, root)) return false;
+    if (root != kBvhEnd) segs.push_back(BvhSegment{0u, root, 0u, 0u});
     i = j;
   }
   return true;
+}
+
+uint32_t bvh_max_depth(const std::vector<BvhSegment>& segs, const std::vector<BvhNode>& nodes) {
+  uint32_t d = 0;
+  for (const BvhSegment& s : segs)
+    if (!s.plane) d = std::max(d, depth_of(nodes, s.root, 0));
+  return d;
 }
 
 }  // namespace fr

@@ -1,13 +1,14 @@
 // Bounding volume hierarchy over a scene's primitives.
 //
-// A threaded ("stackless") binary BVH in depth-first order: an internal node's first
-// child is the next node, and every node carries an escape index, the node after its
-// subtree. A lane walks it with one index: on a box miss or after a leaf it jumps to
-// `escape`, otherwise it steps to the next node. No stack, so no LDS or registers per
-// level. Used only as a conservative cull in front of the primitives' own tests; the
-// closest-hit result is the same as the list-order loop (tracer.rs:195-200) because
-// every primitive's candidate t does not depend on t_max and exact ties are broken by
-// list index (render.hip, the BVH hit loop).
+// A binary BVH whose nodes carry both children's boxes ("child boxes in the parent"):
+// one 64-B fetch gives a lane two independent box tests; it steps into the nearer child
+// it enters and keeps the other on a short per-lane stack in LDS. Leaves are referenced
+// inline by the parent (first leaf slot, count) and their primitives' records are
+// stored in leaf order, so a leaf costs no index hop. Used only as a conservative cull
+// in front of the primitives' own tests; the closest-hit result is the same as the
+// list-order loop (tracer.rs:195-200) because every primitive's candidate t does not
+// depend on t_max and exact ties are broken by list index (render.hip, the BVH hit
+// loop), whatever order the leaves are visited in.
 #ifndef FR_BVH_H
 #define FR_BVH_H
 
@@ -19,44 +20,56 @@
 
 namespace fr {
 
+// Child reference: an internal node index (< kBvhLeaf), a leaf
+// kBvhLeaf | (count - 1) << kBvhSlotBits | first slot, or kBvhEnd.
+constexpr uint32_t kBvhLeaf = 0x80000000u;
+constexpr uint32_t kBvhEnd = 0xFFFFFFFFu;
+constexpr uint32_t kBvhSlotBits = 27;      // leaf slots < 2^27
+constexpr uint32_t kBvhLeafCountMax = 16;  // count field: 4 bits
+constexpr uint32_t bvh_leaf_ref(uint32_t first, uint32_t count) {
+  return kBvhLeaf | ((count - 1u) << kBvhSlotBits) | first;
+}
+
 struct BvhNode {
-  float lo[3];
-  uint32_t escape;  // next node when this box is missed or this leaf is done
-  float hi[3];
-  uint32_t leaf;    // 0: internal (first child = this + 1); else (count << 24) | first
+  float a[4];       // left lo x y z, right lo x
+  float b[4];       // left hi x y z, right hi x
+  float c[4];       // right lo y z, right hi y z
+  uint32_t ref[2];  // left, right child
+  uint32_t pad[2];
 };
-static_assert(sizeof(BvhNode) == 32, "BvhNode is two float4");
+static_assert(sizeof(BvhNode) == 64, "BvhNode is four float4");
 
-constexpr uint32_t kBvhLeafMax = 4;      // primitives per leaf
-constexpr uint32_t kBvhMinPrims = 64;    // smaller scenes keep the in-order loop
+constexpr uint32_t kBvhLeafMax = 4;    // primitives per leaf (more only for huge scenes)
+constexpr uint32_t kBvhMinPrims = 64;  // smaller scenes keep the in-order loop
 // The in-order loop (wave-uniform, scalar loads) beats a divergent per-lane walk until
-// a segment's tests cost enough: weight box / sphere 1, oriented box 2, triangle 2.5
-// (measured: 217 boxes 93 ms in order vs 124 ms BVH; 156 triangles 49 ms vs 19 ms).
+// a segment's tests cost enough: weight box / sphere 1, oriented box 2, triangle 2.5.
 constexpr float kBvhMinCost = 300.0f;
-
-// Builds the BVH over prims[begin, end) (stubs are left out: they never hit), appending
-// its nodes to `nodes` and its leaf primitive indices (global) to `order`; escape and
-// leaf indices are absolute. Returns false (appending nothing) if no primitive of the
-// range can be bounded.
-bool build_bvh(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end, std::vector<BvhNode>& nodes,
-               std::vector<uint32_t>& order);
+// Traversal stack entries per lane (LDS). The builder keeps every internal node at
+// depth < kBvhStack (median splits where SAH would go deeper), and a lane holds at most
+// one entry per internal node on its current path.
+constexpr uint32_t kBvhStack = 16;
 
 // The closest-hit list cut at its planes: runs of consecutive non-plane primitives (one
 // BVH each) and single planes, in list order. A plane hit ignores t_max and may leave
 // a stale record (plane.rs:24-44), so planes are tested one by one where they stand.
 struct BvhSegment {
-  uint32_t plane;       // 1: a plane, prims index `prim`; 0: a run with nodes [first, end)
-  uint32_t first, end;  // node range of the run's tree (end == first: nothing boundable)
+  uint32_t plane;  // 1: a plane, prims index `prim`; 0: a run
+  uint32_t root;   // run: root reference (kBvhEnd: nothing boundable)
+  uint32_t pad;
   uint32_t prim;
 };
 static_assert(sizeof(BvhSegment) == 16, "BvhSegment is one uint4");
 
 constexpr uint32_t kBvhMaxPlanes = 32;  // more planes: the in-order loop
 
-// Segments and trees for a scene; false if the scene is too small or has too many planes
-// (`force` drops the size and cost thresholds, for A/B runs).
+// Segments, nodes and the leaf-order primitive list (`order[slot]` = list index) for a
+// scene; false if the scene is too small, has too many planes or is too large for the
+// reference encoding. `force` drops the size and cost thresholds (A/B runs).
 bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& segs, std::vector<BvhNode>& nodes,
                     std::vector<uint32_t>& order, bool force = false);
+
+// Largest internal-node depth of the trees (root = 0): below kBvhStack by construction.
+uint32_t bvh_max_depth(const std::vector<BvhSegment>& segs, const std::vector<BvhNode>& nodes);
 
 }  // namespace fr
 

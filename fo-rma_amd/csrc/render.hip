@@ -90,8 +90,8 @@ struct DeviceCopy {
   uint32_t kinds = 0;  // bit k set if a primitive of kind k is present
   size_t off_mat = 0, off_cls = 0, off_att = 0;
   size_t off_rec = 0;
-  size_t off_bvh = 0, off_bvh_order = 0, off_segs = 0;
-  uint32_t bvh_n = 0;   // BVH nodes (0 = in-order loop only)
+  size_t off_bvh = 0, off_bvh_order = 0, off_lrec = 0, off_segs = 0;
+  bool bvh_ok = false;  // segments and trees built (else the in-order loop only)
   uint32_t n_segs = 0;  // closest-hit segments: BVH runs and planes (bvh.h)
   bool att_nonneg = true;  // every attenuation component finite and >= +0 (no -0)
 };
@@ -103,12 +103,12 @@ struct KScene {
   const float4* __restrict__ mat;   // colour rgb, fuzz
   const uint32_t* __restrict__ cls; // effective ScatterClass
   const float4* __restrict__ att;   // attenuation rgb (colour, or 1 for light)
-  const float4* __restrict__ bvh;   // BVH nodes, two float4 each (bvh.h), or null
+  const float4* __restrict__ bvh;   // BVH nodes, four float4 each (bvh.h)
   const uint32_t* __restrict__ bvh_order;  // primitive index of each leaf slot
+  const float4* __restrict__ lrec;  // the primitives' records in leaf-slot order
   const uint4* __restrict__ segs;   // BvhSegment list: runs (one tree each) and planes, in list order
   uint32_t n;
-  uint32_t bvh_n;                   // node count (0: no BVH)
-  uint32_t n_segs;                  // segment count
+  uint32_t n_segs;                  // segment count (0: no BVH)
   uint32_t att_nonneg;              // every attenuation component finite and >= +0
 };
 
@@ -330,6 +330,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   const uint32_t lane = tid & 63u;
   static_assert(MAXD == 0 || MAXD == 8, "the u16 stack is one 16-B row per lane");
   uint4* hrow = reinterpret_cast<uint4*>(stack) + tid;  // this lane's MAXD = 8 levels
+  // BVH traversal stack, after the unwind stack: kBvhStack x kBlock u32 (level-major)
+  uint32_t* tstack = stack + (MAXD ? (MAXD * kBlock) / 2u : (kp.max_depth ? kp.max_depth : 1u) * kBlock);
   const uint32_t unit2 = sc.n | (sc.n << 16);            // two empty levels
   if (MAXD > 0) *hrow = make_uint4(unit2, unit2, unit2, unit2);
   for (uint32_t i = tid; i < n_att_st; i += kBlock) {
@@ -523,12 +525,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       int best = -1;
       if (BVH) {
         // The list cut at its planes (bvh.h), walked in list order: each plane tested
-        // where it stands, each run of other primitives through its own threaded tree,
-        // one node index per lane. A primitive's candidate t does not depend on t_max,
-        // so a run's effect is the least (t, index) of the run below `closest`: a
-        // primitive listed before the current winner may take an exact tie, tested with
-        // t_max one ulp above closest. Boxes are padded, so no primitive the list loop
-        // accepts is culled.
+        // where it stands, each run of other primitives through its own tree. A
+        // primitive's candidate t does not depend on t_max, so a run's effect is the
+        // least (t, index) of the run below `closest`: a primitive listed before the
+        // current winner may take an exact tie, tested with t_max one ulp above
+        // closest. Boxes are padded, so no primitive the list loop accepts is culled
+        // (DESIGN.md §4.8). A lane steps into the nearer entered child and stacks the
+        // other; lanes that reach a leaf wait for the wave's others, so leaves are
+        // tested together.
         typedef __attribute__((address_space(4))) const uint32_t cu32;
         for (uint32_t sg = 0; sg < sc.n_segs; ++sg) {
           const cu32* sp = (cu32*)(reinterpret_cast<uintptr_t>(sc.segs)) + 4u * __builtin_amdgcn_readfirstlane(sg);
@@ -544,45 +548,60 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
             }
             continue;
           }
-          uint32_t ni = sp[1];
-          const uint32_t nend = sp[2];
-          while (ni < nend) {
-            const float4 na = sc.bvh[2 * ni], nb = sc.bvh[2 * ni + 1];
-            const Slab sl = slab3(xyz(na), xyz(nb), o, inv);
-            const bool enter = (sl.tn <= sl.tf) & (sl.tf >= 0.001f) & (sl.tn <= closest);
-            const uint32_t leaf = __float_as_uint(nb.w);
-            if (enter && leaf) {
-              const uint32_t first = leaf & 0xFFFFFFu, cnt = leaf >> 24;
-              for (uint32_t kk = 0; kk < cnt; ++kk) {
-                const uint32_t i = sc.bvh_order[first + kk];
-                const float4* r = sc.rec + 4 * i;
-                const float tmax =
-                    static_cast<int>(i) < best ? __uint_as_float(__float_as_uint(closest) + 1u) : closest;
-                const uint32_t k = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(r[3].w);
-                float t = 0.0f;
-                bool h = false;
-                if (k == FR_SPHERE) {
-                  const float4 g = r[0];
-                  h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, tmax, t);
-                } else if (k == FR_AABB) {
-                  h = slab_root(slab3(xyz(r[0]), xyz(r[1]), o, inv), 0.001f, tmax, t);
-                } else if (k == FR_TRIANGLE) {
-                  h = tri_root(xyz(r[0]), xyz(r[1]), xyz(r[2]), o, d, 0.001f, tmax, t);
-                } else if (k == FR_OBB) {
-                  const float4 a = r[0], b = r[1], c = r[2], e = r[3];
-                  const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
-                  h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, tmax, t);
-                }
-                if (h) {
-                  closest = t;
-                  best = static_cast<int>(i);
-                  if (HAS_PLANE) t_last = t;
-                }
+          uint32_t ref = sp[1];
+          uint32_t depth_s = 0;  // entries on this lane's traversal stack
+          while (ref != kBvhEnd) {
+            while (ref < kBvhLeaf) {
+              // internal node: both children's boxes
+              const float4 na = sc.bvh[4 * ref], nb = sc.bvh[4 * ref + 1], nc = sc.bvh[4 * ref + 2];
+              const uint4 nr = reinterpret_cast<const uint4*>(sc.bvh)[4 * ref + 3];
+              const Slab sl = slab3(xyz(na), xyz(nb), o, inv);
+              const Slab sr = slab3(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, o, inv);
+              const bool hl = (sl.tn <= sl.tf) & (sl.tf >= 0.001f) & (sl.tn <= closest);
+              const bool hr = (sr.tn <= sr.tf) & (sr.tf >= 0.001f) & (sr.tn <= closest);
+              if (hl & hr) {
+                const bool lfirst = sl.tn <= sr.tn;
+                tstack[depth_s * kBlock + tid] = lfirst ? nr.y : nr.x;
+                ++depth_s;
+                ref = lfirst ? nr.x : nr.y;
+              } else if (hl | hr) {
+                ref = hl ? nr.x : nr.y;
+              } else {
+                ref = depth_s ? tstack[--depth_s * kBlock + tid] : kBvhEnd;
               }
-              ni = __float_as_uint(na.w);
-            } else {
-              ni = enter ? ni + 1u : __float_as_uint(na.w);
             }
+            if (ref == kBvhEnd) break;
+            // leaf: slots [first, first + count) of the leaf-order records
+            const uint32_t first = ref & ((1u << kBvhSlotBits) - 1u);
+            const uint32_t cnt = ((ref >> kBvhSlotBits) & 15u) + 1u;
+            for (uint32_t kk = 0; kk < cnt; ++kk) {
+              const uint32_t slot = first + kk;
+              const uint32_t i = sc.bvh_order[slot];
+              const float4* r = sc.lrec + 4 * slot;
+              const float tmax =
+                  static_cast<int>(i) < best ? __uint_as_float(__float_as_uint(closest) + 1u) : closest;
+              const uint32_t k = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(r[3].w);
+              float t = 0.0f;
+              bool h = false;
+              if (k == FR_SPHERE) {
+                const float4 g = r[0];
+                h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, tmax, t);
+              } else if (k == FR_AABB) {
+                h = slab_root(slab3(xyz(r[0]), xyz(r[1]), o, inv), 0.001f, tmax, t);
+              } else if (k == FR_TRIANGLE) {
+                h = tri_root(xyz(r[0]), xyz(r[1]), xyz(r[2]), o, d, 0.001f, tmax, t);
+              } else if (k == FR_OBB) {
+                const float4 a = r[0], b = r[1], c = r[2], e = r[3];
+                const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
+                h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, tmax, t);
+              }
+              if (h) {
+                closest = t;
+                best = static_cast<int>(i);
+                if (HAS_PLANE) t_last = t;
+              }
+            }
+            ref = depth_s ? tstack[--depth_s * kBlock + tid] : kBvhEnd;
           }
         }
       }
@@ -911,7 +930,8 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   // FR_BVH=1 builds the BVH below the size/cost thresholds (A/B runs), FR_BVH=0 never uses it
   const char* bvh_env = getenv("FR_BVH");
   const bool force_bvh = bvh_env && strcmp(bvh_env, "1") == 0;
-  if (!build_segments(s->prims, bvh_segs, bvh_nodes, bvh_order, force_bvh)) {
+  const bool bvh_ok = build_segments(s->prims, bvh_segs, bvh_nodes, bvh_order, force_bvh);
+  if (!bvh_ok) {
     bvh_segs.clear();
     bvh_nodes.clear();
     bvh_order.clear();
@@ -929,16 +949,16 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   off = align_up(off + (bvh_nodes.size() ? bvh_nodes.size() : 1) * sizeof(BvhNode), 256);
   c->off_bvh_order = off;
   off = align_up(off + (bvh_order.size() ? bvh_order.size() : 1) * 4, 256);
+  c->off_lrec = off;
+  off = align_up(off + (bvh_order.size() ? bvh_order.size() : 1) * 64, 256);
   c->off_segs = off;
   off = align_up(off + (bvh_segs.size() ? bvh_segs.size() : 1) * sizeof(BvhSegment), 256);
   std::vector<unsigned char> host(off, 0);
   bool nonneg = true;
-  if (!bvh_nodes.empty()) {
-    memcpy(&host[c->off_bvh], bvh_nodes.data(), bvh_nodes.size() * sizeof(BvhNode));
-    memcpy(&host[c->off_bvh_order], bvh_order.data(), bvh_order.size() * 4);
-  }
+  if (!bvh_nodes.empty()) memcpy(&host[c->off_bvh], bvh_nodes.data(), bvh_nodes.size() * sizeof(BvhNode));
+  if (!bvh_order.empty()) memcpy(&host[c->off_bvh_order], bvh_order.data(), bvh_order.size() * 4);
   if (!bvh_segs.empty()) memcpy(&host[c->off_segs], bvh_segs.data(), bvh_segs.size() * sizeof(BvhSegment));
-  c->bvh_n = static_cast<uint32_t>(bvh_nodes.size());
+  c->bvh_ok = bvh_ok;
   c->n_segs = static_cast<uint32_t>(bvh_segs.size());
   for (uint32_t i = 0; i < n; ++i) {
     const fr_prim& p = s->prims[i];
@@ -988,6 +1008,9 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
     memcpy(&host[c->off_rec + 64 * i], g, 64);
   }
   c->att_nonneg = nonneg;
+  // the BVH leaves' records, in leaf-slot order
+  for (size_t slot = 0; slot < bvh_order.size(); ++slot)
+    memcpy(&host[c->off_lrec + 64 * slot], &host[c->off_rec + 64 * static_cast<size_t>(bvh_order[slot])], 64);
   {
     // entry n: the unit attenuation the depth-8 stack's empty levels point at
     const float4 one = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
@@ -1213,10 +1236,10 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   ks.n = dc->n;
   // FR_BVH=0 forces the in-order loop (A/B and tests)
   const char* bvh_env = getenv("FR_BVH");
-  const bool use_bvh = dc->bvh_n > 0 && !(bvh_env && strcmp(bvh_env, "0") == 0);
+  const bool use_bvh = dc->bvh_ok && dc->n_segs > 0 && !(bvh_env && strcmp(bvh_env, "0") == 0);
   ks.bvh = reinterpret_cast<const float4*>(b + dc->off_bvh);
   ks.bvh_order = reinterpret_cast<const uint32_t*>(b + dc->off_bvh_order);
-  ks.bvh_n = use_bvh ? dc->bvh_n : 0u;
+  ks.lrec = reinterpret_cast<const float4*>(b + dc->off_lrec);
   ks.segs = reinterpret_cast<const uint4*>(b + dc->off_segs);
   ks.n_segs = use_bvh ? dc->n_segs : 0u;
   ks.att_nonneg = dc->att_nonneg ? 1u : 0u;
@@ -1303,7 +1326,8 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
                                          : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
                                                sizeof(uint32_t);
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
-  const size_t lds = (n_att ? n_att + 1 : 0) * 16 + n_rec * 64 + stack_bytes;
+  const size_t lds = (n_att ? n_att + 1 : 0) * 16 + n_rec * 64 + stack_bytes +
+                     (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
   KWork kw;
   kw.counters = c->d_cnt;
   c->t0 = std::chrono::steady_clock::now();

@@ -562,3 +562,42 @@ def test_absorbed_path_through_infinite_attenuation_is_nan(gpu, depth):
     assert _same_bits(mean, omean)
     assert np.array_equal(u8, ou8)
     assert (st["segments"], st["hits"]) == (ocnt["segments"], ocnt["hits"])
+
+
+def test_bvh_depth_cap_chain_scene(gpu, monkeypatch):
+    """Spheres at exponentially growing distances: binned SAH peels a few off per level,
+    so the builder must switch to median splits to keep every internal node within the
+    kBvhStack-entry traversal stack (bvh.h). Checked against the list-order loop and
+    the oracle."""
+    prims = []
+    for k in range(700):
+        x = 1.02 ** k - 1.0
+        prims.append(S.sphere((x - 3.0, 0.3 * np.sin(k), -3.0 - 0.01 * k), 0.05 + 0.002 * (k % 7), k % 4,
+                              (0.2 + 0.001 * k, 0.5, 0.7), 0.3))
+    prims.append(S.sphere((0.0, -1000.5, -1.0), 1000.0, 0, (0.5, 0.5, 0.5), 0.0))
+    w, h, spp, depth = 40, 24, 2, 8
+    cam = gpu.camera_new(w, h)
+    mean, u8, st = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=5)
+    omean, ou8, ocnt, _ = O.render(prims, O.camera_new(w, h), w, h, spp, depth, seed=5, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    monkeypatch.setenv("FR_BVH", "0")
+    mean0, _, st0 = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=5)
+    assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
+
+
+def test_bvh_at_the_depth_cap_matches_list_loop(gpu, monkeypatch):
+    """150k spheres: leaves grow past kBvhLeafMax and the deepest internal node sits at
+    the traversal stack's limit (bvh.cpp). The BVH result must equal the list-order loop
+    bit for bit (the oracle is too slow at this size; the loop is pinned to it above)."""
+    r = np.random.default_rng(11)
+    c = r.uniform(-40, 40, (150000, 3)) * np.array([1.0, 0.15, 1.0]) + np.array([0, 0, -45.0])
+    rad = r.uniform(0.05, 0.3, 150000)
+    mats = r.integers(0, 4, 150000)
+    prims = [S.sphere(c[k], rad[k], int(mats[k]), (0.6, 0.5, 0.4), 0.2) for k in range(len(c))]
+    w, h, spp, depth = 32, 18, 1, 8
+    cam = gpu.camera_new(w, h)
+    mean, u8, st = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=9)
+    assert st["hits"] > 0
+    monkeypatch.setenv("FR_BVH", "0")
+    mean0, _, st0 = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=9)
+    assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
