@@ -250,7 +250,7 @@ uint32_t depth_of(const std::vector<BvhNode>& nodes, uint32_t ref, uint32_t dept
 }  // namespace
 
 bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& segs, std::vector<BvhNode>& nodes,
-                    std::vector<uint32_t>& order, bool force) {
+                    std::vector<uint32_t>& order, bool force, float* extent) {
   segs.clear();
   nodes.clear();
   order.clear();
@@ -264,7 +264,9 @@ bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& 
   if (!force && (n < kBvhMinPrims || cost < kBvhMinCost)) return false;
   // The cull must never reject a primitive whose own test accepts a hit: pad every box
   // by a margin far above the f32 error of a root or a slab distance at scene scale.
-  const float pad = 1e-4f * scene_abs_max(prims) + 1e-4f;
+  const float ext = scene_abs_max(prims);
+  if (extent) *extent = ext;
+  const float pad = 1e-4f * ext + 1e-4f;
   uint32_t i = 0;
   while (i < n) {
     if (prims[i].kind == FR_PLANE) {

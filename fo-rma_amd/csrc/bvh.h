@@ -40,10 +40,12 @@ struct BvhNode {
 static_assert(sizeof(BvhNode) == 64, "BvhNode is four float4");
 
 constexpr uint32_t kBvhLeafMax = 4;    // primitives per leaf (more only for huge scenes)
-constexpr uint32_t kBvhMinPrims = 64;  // smaller scenes keep the in-order loop
-// The in-order loop (wave-uniform, scalar loads) beats a divergent per-lane walk until
-// a segment's tests cost enough: weight box / sphere 1, oriented box 2, triangle 2.5.
-constexpr float kBvhMinCost = 300.0f;
+// The in-order loop (wave-uniform, scalar loads) beats the per-lane walk only for small
+// lists: weight box / sphere 1, oriented box 2, triangle 2.5. Measured at 1080p
+// (tools/bvh_threshold.sh): 43 mixed prims (scene_01) 38 ms in order vs 55 BVH; 50
+// spheres 6.4 vs 5.1; 50 oriented boxes 17.9 vs 9.4; 74 (scene_05) 32.6 vs 27.1.
+constexpr uint32_t kBvhMinPrims = 48;  // smaller scenes keep the in-order loop
+constexpr float kBvhMinCost = 48.0f;
 // Traversal stack entries per lane (LDS). The builder keeps every internal node at
 // depth < kBvhStack (median splits where SAH would go deeper), and a lane holds at most
 // one entry per internal node on its current path.
@@ -65,8 +67,15 @@ constexpr uint32_t kBvhMaxPlanes = 32;  // more planes: the in-order loop
 // Segments, nodes and the leaf-order primitive list (`order[slot]` = list index) for a
 // scene; false if the scene is too small, has too many planes or is too large for the
 // reference encoding. `force` drops the size and cost thresholds (A/B runs).
+// `extent` (if given) receives the largest |coordinate| of any primitive's bounds: the
+// boxes are padded by 1e-4 * (extent + 1).
 bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& segs, std::vector<BvhNode>& nodes,
-                    std::vector<uint32_t>& order, bool force = false);
+                    std::vector<uint32_t>& order, bool force = false, float* extent = nullptr);
+
+// Ray origins the node cull is conservative for: |o| <= kBvhOriginReach * (extent + 1)
+// (the kernel's fused node slabs add |o| 2^-24 to a slab distance; the padding allows
+// 2^24 * 1e-4 = 1677 times that). A camera farther out renders with the in-order loop.
+constexpr float kBvhOriginReach = 100.0f;
 
 // Largest internal-node depth of the trees (root = 0): below kBvhStack by construction.
 uint32_t bvh_max_depth(const std::vector<BvhSegment>& segs, const std::vector<BvhNode>& nodes);

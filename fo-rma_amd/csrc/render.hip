@@ -92,6 +92,7 @@ struct DeviceCopy {
   size_t off_rec = 0;
   size_t off_bvh = 0, off_bvh_order = 0, off_lrec = 0, off_segs = 0;
   bool bvh_ok = false;  // segments and trees built (else the in-order loop only)
+  float bvh_extent = 0; // largest |coordinate| of the primitives' bounds (bvh.h)
   uint32_t n_segs = 0;  // closest-hit segments: BVH runs and planes (bvh.h)
   bool att_nonneg = true;  // every attenuation component finite and >= +0 (no -0)
 };
@@ -213,7 +214,7 @@ constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for smal
 // and lane-level work, to measure SIMT efficiency. Never enabled in the product.
 #ifdef FR_DIAG
 enum { DG_ITER, DG_REGEN_W, DG_REGEN_L, DG_LENS_W, DG_LENS_L, DG_RUS_W, DG_RUS_L, DG_END_W, DG_END_L,
-       DG_UNW_W, DG_UNW_L, DG_HIT_W, DG_N };
+       DG_UNW_W, DG_UNW_L, DG_HIT_W, DG_NODE_W, DG_NODE_L, DG_LEAF_W, DG_LEAF_L, DG_N };
 #define DIAG_WAVE(slot)                                                         \
   do {                                                                          \
     const unsigned long long m_ = __ballot(1);                                  \
@@ -550,13 +551,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           }
           uint32_t ref = sp[1];
           uint32_t depth_s = 0;  // entries on this lane's traversal stack
+          // node slabs as fma(lo, inv, -o inv): a cull only, covered by the padding for
+          // origins within kBvhOriginReach scene extents (bvh.h; the host checks the camera)
+          const V3 oinv{o.x * inv.x, o.y * inv.y, o.z * inv.z};
           while (ref != kBvhEnd) {
             while (ref < kBvhLeaf) {
+              DIAG_WAVE(DG_NODE_W);
+              DIAG_LANE(DG_NODE_L);
               // internal node: both children's boxes
               const float4 na = sc.bvh[4 * ref], nb = sc.bvh[4 * ref + 1], nc = sc.bvh[4 * ref + 2];
               const uint4 nr = reinterpret_cast<const uint4*>(sc.bvh)[4 * ref + 3];
-              const Slab sl = slab3(xyz(na), xyz(nb), o, inv);
-              const Slab sr = slab3(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, o, inv);
+              const Slab sl = slab3_fused(xyz(na), xyz(nb), oinv, inv);
+              const Slab sr = slab3_fused(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, oinv, inv);
               const bool hl = (sl.tn <= sl.tf) & (sl.tf >= 0.001f) & (sl.tn <= closest);
               const bool hr = (sr.tn <= sr.tf) & (sr.tf >= 0.001f) & (sr.tn <= closest);
               if (hl & hr) {
@@ -571,6 +577,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               }
             }
             if (ref == kBvhEnd) break;
+            DIAG_WAVE(DG_LEAF_W);
+            DIAG_LANE(DG_LEAF_L);
             // leaf: slots [first, first + count) of the leaf-order records
             const uint32_t first = ref & ((1u << kBvhSlotBits) - 1u);
             const uint32_t cnt = ((ref >> kBvhSlotBits) & 15u) + 1u;
@@ -930,7 +938,8 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   // FR_BVH=1 builds the BVH below the size/cost thresholds (A/B runs), FR_BVH=0 never uses it
   const char* bvh_env = getenv("FR_BVH");
   const bool force_bvh = bvh_env && strcmp(bvh_env, "1") == 0;
-  const bool bvh_ok = build_segments(s->prims, bvh_segs, bvh_nodes, bvh_order, force_bvh);
+  float bvh_extent = 0.0f;
+  const bool bvh_ok = build_segments(s->prims, bvh_segs, bvh_nodes, bvh_order, force_bvh, &bvh_extent);
   if (!bvh_ok) {
     bvh_segs.clear();
     bvh_nodes.clear();
@@ -959,6 +968,7 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   if (!bvh_order.empty()) memcpy(&host[c->off_bvh_order], bvh_order.data(), bvh_order.size() * 4);
   if (!bvh_segs.empty()) memcpy(&host[c->off_segs], bvh_segs.data(), bvh_segs.size() * sizeof(BvhSegment));
   c->bvh_ok = bvh_ok;
+  c->bvh_extent = bvh_extent;
   c->n_segs = static_cast<uint32_t>(bvh_segs.size());
   for (uint32_t i = 0; i < n; ++i) {
     const fr_prim& p = s->prims[i];
@@ -1236,7 +1246,11 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   ks.n = dc->n;
   // FR_BVH=0 forces the in-order loop (A/B and tests)
   const char* bvh_env = getenv("FR_BVH");
-  const bool use_bvh = dc->bvh_ok && dc->n_segs > 0 && !(bvh_env && strcmp(bvh_env, "0") == 0);
+  // the node cull holds for origins within kBvhOriginReach scene extents (bvh.h)
+  const float cam_reach = std::max(std::max(fabsf(cam->position[0]), fabsf(cam->position[1])),
+                                   fabsf(cam->position[2])) + fabsf(cam->lens_radius);
+  const bool cam_near = cam_reach <= kBvhOriginReach * (dc->bvh_extent + 1.0f);
+  const bool use_bvh = dc->bvh_ok && dc->n_segs > 0 && cam_near && !(bvh_env && strcmp(bvh_env, "0") == 0);
   ks.bvh = reinterpret_cast<const float4*>(b + dc->off_bvh);
   ks.bvh_order = reinterpret_cast<const uint32_t*>(b + dc->off_bvh_order);
   ks.lrec = reinterpret_cast<const float4*>(b + dc->off_lrec);
@@ -1409,10 +1423,11 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
             "FR_DIAG {\"iter_w\": %llu, \"regen_w\": %llu, \"regen_l\": %llu, \"hit_w\": %llu, \"end_w\": %llu, "
             "\"end_l\": %llu, \"unwind_w\": %llu, \"unwind_l\": %llu, \"lens_w\": %llu, \"lens_l\": %llu, "
             "\"rus_w\": %llu, \"rus_l\": %llu, \"merged_w\": %llu, \"merged_l\": %llu, \"segments\": %llu, "
-            "\"hits\": %llu}\n",
+            "\"hits\": %llu, \"node_w\": %llu, \"node_l\": %llu, \"leaf_w\": %llu, \"leaf_l\": %llu}\n",
             cnt[4 + DG_ITER], cnt[4 + DG_REGEN_W], cnt[4 + DG_REGEN_L], cnt[4 + DG_HIT_W], cnt[4 + DG_END_W],
             cnt[4 + DG_END_L], cnt[4 + DG_UNW_W], cnt[4 + DG_UNW_L], dl[0], dl[1], dr[0], dr[1], cnt[4 + DG_LENS_W],
-            cnt[4 + DG_LENS_L], cnt[0], cnt[1]);
+            cnt[4 + DG_LENS_L], cnt[0], cnt[1], cnt[4 + DG_NODE_W], cnt[4 + DG_NODE_L], cnt[4 + DG_LEAF_W],
+            cnt[4 + DG_LEAF_L]);
     if (const char* path = getenv("FR_DIAG_TIMES")) {
       std::vector<unsigned long long> wt(2 * 65536);
       HIPCHK(hipMemcpyFromSymbol(wt.data(), HIP_SYMBOL(g_fr_wave_times), wt.size() * 8));

@@ -269,6 +269,17 @@ FR_HD Slab slab3(V3 lo, V3 hi, V3 o, V3 inv) {
   return s;
 }
 
+// The same slab distances as fma(lo, inv, -o inv) with oinv = o inv precomputed: not
+// the box primitive's exact arithmetic, only for the BVH's padded cull boxes (bvh.h).
+FR_HD Slab slab3_fused(V3 lo, V3 hi, V3 oinv, V3 inv) {
+  Slab s;
+  s.t0 = V3{fmaf(lo.x, inv.x, -oinv.x), fmaf(lo.y, inv.y, -oinv.y), fmaf(lo.z, inv.z, -oinv.z)};
+  s.t1 = V3{fmaf(hi.x, inv.x, -oinv.x), fmaf(hi.y, inv.y, -oinv.y), fmaf(hi.z, inv.z, -oinv.z)};
+  s.tn = fmax3_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y), fmin_num(s.t0.z, s.t1.z));
+  s.tf = fmin_num(fmin_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y)), fmax_num(s.t0.z, s.t1.z));
+  return s;
+}
+
 // Root selection: returns true and the accepted t if the box is hit in (t_min, t_max).
 // Equivalent branch-free form of "near root if tn in (t_min, t_max), else far root if
 // tf in (t_min, t_max), and tn < tf": when tn > t_min the far root can only be taken

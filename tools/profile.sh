@@ -1,5 +1,6 @@
 #!/bin/bash
-# rocprofv3 collection for the bench workload (run on the GPU box via gpurun).
+# rocprofv3 collection for the bench workload (run on the GPU box via gpurun), or for
+# PROF_CMD (a python3 command line, e.g. "python3 tools/time_config.py scene_04 1920 1080 64 8 1").
 # Kernel trace + stats in one run; each PMC group in its own run (never combined
 # with sys/runtime traces). Output under gpurun_out/prof/<tag>/.
 tag="${1:-r01}"
@@ -7,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 out="gpurun_out/prof/$tag"
 mkdir -p "$out"
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+B="${PROF_CMD:-python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline}"
 run() {  # name seconds args...
   local name=$1 secs=$2; shift 2
   echo "=== $name"
