@@ -613,9 +613,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           }
         }
       }
-#ifdef FR_HIT_UNROLL
-#pragma unroll FR_HIT_UNROLL
-#endif
       for (uint32_t ii = 0; ii < (BVH ? 0u : sc.n); ++ii) {
         // the index is wave-uniform; say so, or the compiler may fall back to vector loads
         const uint32_t i = __builtin_amdgcn_readfirstlane(ii);
