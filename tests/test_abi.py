@@ -23,7 +23,7 @@ def test_every_declared_symbol_is_exported(fr):
 
 
 def test_abi_version_and_struct_sizes(fr):
-    assert fr.lib().fr_abi_version() == 2
+    assert fr.lib().fr_abi_version() == fr.FR_ABI_VERSION == 2
     assert C.sizeof(fr.FrPrim) == 88
     assert C.sizeof(fr.FrCamera) == 26 * 4
     assert C.sizeof(fr.FrParams) == 40  # static_assert-ed in render.hip
@@ -51,3 +51,9 @@ def test_render_without_device_fails_loudly(fr):
         assert e.code in (fr.FR_ENODEV, fr.FR_EHIP)
     else:
         raise AssertionError("render returned without a GPU")
+
+
+def test_header_abi_version_matches_host_mirror(fr):
+    hdr = open(HEADER).read()
+    m = re.search(r"#define FR_ABI_VERSION (\d+)", hdr)
+    assert m and int(m.group(1)) == fr.FR_ABI_VERSION == fr.lib().fr_abi_version()
