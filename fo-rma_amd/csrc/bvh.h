@@ -76,6 +76,11 @@ bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& 
 // (the kernel's fused node slabs add |o| 2^-24 to a slab distance; the padding allows
 // 2^24 * 1e-4 = 1677 times that). A camera farther out renders with the in-order loop.
 constexpr float kBvhOriginReach = 100.0f;
+// The node cull's reciprocal direction is clamped to [-kBvhInvClamp, kBvhInvClamp]: a
+// zero direction component (inv = +-inf) would make fma(lo, inv, -o inv) NaN. A clamped
+// slab is still conservative: a hit inside a box padded by >= 1e-4 keeps that axis's
+// slab >= 1e-4 * 2^100 ~ 1e26 wide, and |o| 2^100 stays finite.
+constexpr float kBvhInvClamp = 0x1p100f;
 
 // Largest internal-node depth of the trees (root = 0): below kBvhStack by construction.
 uint32_t bvh_max_depth(const std::vector<BvhSegment>& segs, const std::vector<BvhNode>& nodes);

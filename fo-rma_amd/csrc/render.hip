@@ -552,8 +552,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           uint32_t ref = sp[1];
           uint32_t depth_s = 0;  // entries on this lane's traversal stack
           // node slabs as fma(lo, inv, -o inv): a cull only, covered by the padding for
-          // origins within kBvhOriginReach scene extents (bvh.h; the host checks the camera)
-          const V3 oinv{o.x * inv.x, o.y * inv.y, o.z * inv.z};
+          // origins within kBvhOriginReach scene extents (bvh.h; the host checks the camera).
+          // The cull's reciprocal is clamped to +-2^100 (bvh.h kBvhInvClamp): an exact-zero
+          // direction component (a lambertian bounce ((p + n) + r) - p at |p| ~ 5000 gives one
+          // every few thousand scatters) has inv = +-inf, and fma(lo, inf, -(o inf)) is
+          // inf - inf = NaN, which culled boxes the ray is inside. With the clamp, o inv is
+          // finite and a slab that holds the ray's hit by the padding (>= 1e-4) stays
+          // >= 1e-4 * 2^100 wide on that axis.
+          const V3 invc{__builtin_amdgcn_fmed3f(inv.x, -kBvhInvClamp, kBvhInvClamp),
+                        __builtin_amdgcn_fmed3f(inv.y, -kBvhInvClamp, kBvhInvClamp),
+                        __builtin_amdgcn_fmed3f(inv.z, -kBvhInvClamp, kBvhInvClamp)};
+          const V3 oinv{o.x * invc.x, o.y * invc.y, o.z * invc.z};
           while (ref != kBvhEnd) {
             while (ref < kBvhLeaf) {
               DIAG_WAVE(DG_NODE_W);
@@ -561,8 +570,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               // internal node: both children's boxes
               const float4 na = sc.bvh[4 * ref], nb = sc.bvh[4 * ref + 1], nc = sc.bvh[4 * ref + 2];
               const uint4 nr = reinterpret_cast<const uint4*>(sc.bvh)[4 * ref + 3];
-              const Slab sl = slab3_fused(xyz(na), xyz(nb), oinv, inv);
-              const Slab sr = slab3_fused(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, oinv, inv);
+              const Slab sl = slab3_fused(xyz(na), xyz(nb), oinv, invc);
+              const Slab sr = slab3_fused(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, oinv, invc);
               const bool hl = (sl.tn <= sl.tf) & (sl.tf >= 0.001f) & (sl.tn <= closest);
               const bool hr = (sr.tn <= sr.tf) & (sr.tf >= 0.001f) & (sr.tn <= closest);
               if (hl & hr) {

@@ -449,6 +449,37 @@ def test_bvh_generator_10k_spheres_small(gpu):
     assert st["hits"] > 0
 
 
+def test_bvh_far_scene_axis_parallel_bounces(gpu, monkeypatch):
+    """A scene ~40000 units from the origin: a lambertian bounce ((p + n) + r) - p there has
+    an exact-zero direction component every few hundred scatters (ulp(p) = 2^-8), so 1/d
+    is +-inf. The node cull must keep boxes such a ray is inside (render.hip clamps the
+    cull's reciprocal, bvh.h kBvhInvClamp); C5's spheres at y ~ 5000 hit the same case."""
+    r = np.random.default_rng(11)
+    base = np.array([40000.0, 40000.0, 40000.0])
+    prims = []
+    for i in range(7):
+        for j in range(7):
+            for k in range(6):
+                c = base + np.array([4.0 * i - 12, 4.0 * j - 12, 4.0 * k + 10]) + r.uniform(-0.5, 0.5, 3)
+                mat = int(r.choice([0, 0, 0, 1, 2]))
+                if (i + j + k) % 3 == 0:
+                    h = r.uniform(0.6, 1.6, 3)
+                    prims.append(S.prim(S.AABB, mat, r.uniform(0.2, 1.0, 3), 0.2, list(c - h) + list(c + h)))
+                else:
+                    prims.append(S.sphere(c, float(r.uniform(0.8, 1.7)), mat, r.uniform(0.2, 1.0, 3), 0.2))
+    w, h, spp, depth = 48, 32, 4, 8
+    frm, at, vup = base, base + np.array([0.0, 0.0, 1.0]), np.array([0.0, 1.0, 0.0])
+    sc = gpu.Scene.from_prims(prims)
+    cam = gpu.camera_look(frm, at, vup, 70.0, 0.1, w, h)
+    mean, u8, st = gpu.render(sc, cam, w, h, spp, depth, seed=5)
+    omean, ou8, ocnt, _ = O.render(prims, O.camera_look(frm, at, vup, 70.0, 0.1, w, h), w, h, spp, depth,
+                                   seed=5, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    monkeypatch.setenv("FR_BVH", "0")
+    mean0, _, st0 = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=5)
+    assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
+
+
 # ---- save_image_mt (tracer.rs:83-158) ---------------------------------------------
 
 @pytest.mark.parametrize("which,w,h,sample", [(0, 32, 18, 3), (0, 40, 24, 1), (2, 36, 22, 20), (0, 16, 3, 2)])
