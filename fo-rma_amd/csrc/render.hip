@@ -12,7 +12,7 @@
 //
 // Closest hit: small scenes test primitive i on every lane at once (wave-uniform:
 // the kind switch is a scalar branch, records arrive by scalar loads); large ones
-// walk a threaded BVH per lane, cut at the planes (bvh.h). Layout and rooflines:
+// walk a BVH per lane (LDS stack), cut at the planes (bvh.h). Layout and rooflines:
 // DESIGN.md §4-§5.
 #include <hip/hip_runtime.h>
 #include <float.h>
@@ -68,12 +68,9 @@ constexpr uint32_t kSmallDepth = 8;
 #define FR_BLOCK_SAMPLES 16  // RNG contract: one stream per 16-sample block (oracle.cpp agrees)
 #endif
 constexpr uint32_t kBlockSamples = FR_BLOCK_SAMPLES;  // samples per RNG stream (numerics contract)
-#ifndef FR_BATCH
-#define FR_BATCH 64
-#endif
-// work items reserved per step of the global counter (a claim reserves whole steps)
-constexpr uint32_t kBatch = FR_BATCH;
-static_assert(kBatch >= 1 && kBatch <= 64 && (kBatch & (kBatch - 1)) == 0, "kBatch: power of two <= 64");
+// work items reserved per step of the global counter: one tile of one sample block,
+// seeded by the wave's 64 lanes at once (trace_kernel's claim step)
+constexpr uint32_t kBatch = 64;
 
 // ABI layout, mirrored by ctypes (forma_rt.py) and the Rust binding
 static_assert(sizeof(fr_prim) == 88, "fr_prim layout");
@@ -385,12 +382,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // the wave's claimed item batch [q_next, q_end): wave-uniform, updated only under
   // the uniform branch below, so it lives in scalar registers
   uint32_t q_next = 0, q_end = 0;
+  // Stream starts of the wave's batch: lane k holds item (batch base + k)'s. The whole
+  // wave seeds a batch when it reserves one, so rng_seed (16 quarter-rate 32-bit
+  // multiplies) runs once per 64 items at full width instead of in every iteration in
+  // which a lane or two claim; a claiming lane fetches its stream by a lane permute.
+  Rng held{0u, 0u, 0u, 0u};
   while (active) {
     DIAG_WAVE(DG_ITER);
     const unsigned long long m = __ballot(need_item);
     if (m) {
       // 0. claim work items: the free lanes take consecutive items of the wave's batch;
-      // when it runs out, the first free lane claims the next kBatch-multiple globally.
+      // when it runs out, the first free lane reserves the next batch of kBatch = 64
+      // items (one tile of one sample block) globally. n <= 64, so one batch suffices.
       // (Prefetching the next item in batched refill passes measured slower.)
       const uint32_t n = static_cast<uint32_t>(__popcll(m));
       const uint32_t r = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
@@ -398,16 +401,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       const uint32_t next = __builtin_amdgcn_readfirstlane(q_next);
       const uint32_t avail = __builtin_amdgcn_readfirstlane(q_end) - next;
       uint32_t base = 0;
-      // the lanes past the wave's batch need `want` items: reserve whole kBatch steps
-      const uint32_t grab = n > avail ? (n - avail + kBatch - 1u) & ~(kBatch - 1u) : 0u;
+      const bool grab = n > avail;
       const int first = __ffsll(static_cast<long long>(m)) - 1;
+      Rng src = held;  // slots [64 - avail, 64) still hold the current batch's streams
       if (grab) {
-        if (static_cast<int>(lane) == first) base = atomicAdd(kw.queue, grab);
+        if (static_cast<int>(lane) == first) base = atomicAdd(kw.queue, kBatch);
         base = __builtin_amdgcn_readlane(base, first);
-        q_end = base + grab;
+        q_end = base + kBatch;
+        // Every lane of the wave is here: a lane retires only after the queue has
+        // drained, and from then on no batch holds a valid item. A slot past the image
+        // or the queue gets a stream that is never used.
+        uint32_t bb, qq, xx, yy;
+        item_xy(kp, base + lane, bb, qq, xx, yy);
+        held = rng_seed(kp.seed, yy * kp.W + xx, bb);
+        if (lane < kBatch - avail) src = held;  // the new batch's first slots are taken now
       }
       q_next = grab ? base + (n - avail) : next + n;
       const uint32_t item = r < avail ? next + r : base + (r - avail);
+      // the item's stream start, from the lane that seeded it (before any lane retires)
+      const int sl = static_cast<int>((item & (kBatch - 1u)) << 2);
+      const Rng st{static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s0))),
+                   static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s1))),
+                   static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s2))),
+                   static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s3)))};
       if (need_item && item >= kp.n_items) {
 #ifdef FR_DIAG
         if (gw < 65536) atomicMin(&g_fr_wave_drain[gw], static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
@@ -428,7 +444,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           vofs = static_cast<float>(3u - k) * 0.25f;
         }
         if (ok) {
-          rng = rng_seed(kp.seed, y * kp.W + x, b);  // this block's stream
+          rng = st;  // this block's stream: rng_seed(seed, y * W + x, b)
           s = b * kBlockSamples;
           out = kw.samples + 3 * (static_cast<size_t>(s - s_pass) * kp.P + q);
           s_end = min(s + kBlockSamples, kp.spp);
