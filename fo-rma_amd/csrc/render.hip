@@ -121,6 +121,7 @@ struct KParams {
   float rW, rH;                       // RN(1 / W), RN(1 / H) (host IEEE division)
   uint32_t row_magic, row_shift;      // x / tiles_per_row = fastdiv(x, row_magic, row_shift)
   uint32_t band_h;                    // FR_FLAG_MT_BANDS: rows per band, H / 4 (tracer.rs:87)
+  uint32_t prio_at[3];  // a wave reserving a batch at or past prio_at[k] raises its priority to k + 1
 };
 
 // Unsigned 32-bit division by the invariant n_tiles: q = (t + ((x - t) >> s1)) >> s2 with
@@ -415,6 +416,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         item_xy(kp, base + lane, bb, qq, xx, yy);
         held = rng_seed(kp.seed, yy * kp.W + xx, bb);
         if (lane < kBatch - avail) src = held;  // the new batch's first slots are taken now
+        // Queue tail: the waves that claim last hold the longest remaining work, so they
+        // get issue priority over waves finishing older items (shortens the drain).
+        if (base >= kp.prio_at[0]) {
+          if (base >= kp.prio_at[2]) __builtin_amdgcn_s_setprio(3);
+          else if (base >= kp.prio_at[1]) __builtin_amdgcn_s_setprio(2);
+          else __builtin_amdgcn_s_setprio(1);
+        }
       }
       q_next = grab ? base + (n - avail) : next + n;
       const uint32_t item = r < avail ? next + r : base + (r - avail);
@@ -1311,6 +1319,9 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   // on C3, but overlapping launches blur each launch's own HIP-event time (DESIGN.md
   // §4.5a), so one pass is the default.
   const size_t per_block = static_cast<size_t>(kp.P) * kBlockSamples * 3 * sizeof(float);
+  // FR_TAIL_PRIO=d: priority from the last 1/d, 1/(4d), 1/(16d) of the queue (0: off)
+  uint32_t tail_prio = 8;
+  if (const char* e = getenv("FR_TAIL_PRIO")) tail_prio = static_cast<uint32_t>(atoi(e) > 0 ? atoi(e) : 0);
   uint32_t want_passes = 1;
   if (const char* e = getenv("FR_PIPELINE")) want_passes = static_cast<uint32_t>(atoi(e) > 0 ? atoi(e) : 1);
   uint32_t passes_u = nblocks ? (want_passes < nblocks ? want_passes : nblocks) : 0u;
@@ -1389,6 +1400,8 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
     kp.b0 = static_cast<uint32_t>(pass) * nb_pass;
     kp.nb = pass < passes ? min(nb_pass, nblocks - kp.b0) : 0u;
     kp.n_items = kp.nb * kp.P;
+    for (int k = 0; k < 3; ++k)
+      kp.prio_at[k] = tail_prio ? kp.n_items - kp.n_items / (tail_prio << (2 * k)) : 0xFFFFFFFFu;
     if (kp.n_items) {
       if (pass >= 2) HIPCHK(hipStreamWaitEvent(ts, c->ev_sum[pass - 2], 0));  // the slot's last reader is done
       kw.queue = reinterpret_cast<uint32_t*>(c->d_cnt + 31 - slot);
