@@ -5,18 +5,34 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-One process per GPU. A step renders the whole frame: rank r renders the 8-row strips
-k with k % N == r (no collective on the data path; each rank's output lands in its own
-device buffer). The timed region is K steps bracketed by a barrier and a device
-synchronize on both sides; the time is the max over ranks; value = all samples of the
-K frames / that time. Inputs (scene, camera) are resident on the device before timing.
-Rank 0 prints one JSON line, with the roofline of the trace kernel (HIP-event time on
-its own stream) and, at N=1, the oracle CPU baseline timed on a bounded row sample.
+One process per GPU. A step renders the whole frame and gathers it to the host: rank r
+renders the 8-row strips k with k % N == r (no collective on the data path) and copies
+its strips (f32 means and the u8 image) into page-locked host memory, the "final gather
+to host" (BASELINE.md §4). The gather of frame k runs on its own stream while frame k+1
+traces; the timed region ends only when the last frame's gather has landed. The timed
+region is K steps bracketed by a barrier and a device synchronize on both sides; the
+time is the max over ranks; value = all samples of the K frames / that time. Inputs
+(scene, camera) are resident on the device before timing.
+
+Rank 0 prints one JSON line with:
+- render_only_*: the same frames by the render's own HIP-event time (no gather);
+- roofline: the trace kernel's binding bound, FP32 VALU: algorithmic FLOP/s (constants
+  frozen in fo-rma_amd/csrc/flops.h, times the kernel's exact counters) against the
+  157.3 TFLOP/s peak, plus the VALU issue fraction and HBM traffic read from rocprofv3
+  hardware counters in this run (a child process, N=1 only);
+- hbm_roofline: algorithmic bytes per launch against 8 TB/s (the north star's ask);
+- cpu_baseline (N=1): the oracle on this host's cores, all of them and one.
 """
 import argparse
+import glob
 import json
 import os
+import re
+import shutil
+import signal
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -27,7 +43,8 @@ SCENE = "scene_08"
 WIDTH, HEIGHT, SPP, DEPTH, SEED = 1920, 1080, 256, 8, 0x5EED
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, chip-level parameters (spec)
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, peak FP32 vector (spec)
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_trace_kernel.json")
+N_SIMDS = 1024             # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles
+FLOPS_H = os.path.join(ROOT, "fo-rma_amd", "csrc", "flops.h")
 
 
 def dist_env():
@@ -43,11 +60,10 @@ def shard_rows(height, shard, shards, strip=8):
 
 
 def gather_frame(mean_rgb, rank, world, height, strip=8):
-    """Stitch every rank's strips into rank 0's image (the optional final gather,
-    outside the timed region). `mean_rgb` is this rank's full-size [H, W, 3] buffer with
-    only its own strips valid. Returns the stitched frame on rank 0, None elsewhere."""
+    """Stitch every rank's strips into rank 0's image (--verify only, after timing).
+    `mean_rgb` is this rank's full-size [H, W, 3] buffer with only its own strips valid.
+    Returns the stitched frame on rank 0, None elsewhere."""
     import numpy as np
-    import torch
     import torch.distributed as dist
 
     if world == 1:
@@ -63,22 +79,183 @@ def gather_frame(mean_rgb, rank, world, height, strip=8):
     return out
 
 
+# ---- algorithmic work model ----------------------------------------------------
+
+def flop_constants(path=FLOPS_H):
+    """The `constexpr double kFlop...` / `k...Tries` constants of flops.h, evaluated in
+    order (later ones may use earlier ones)."""
+    consts = {}
+    for name, expr in re.findall(r"constexpr double (k\w+) = ([^;]+);", open(path).read()):
+        consts[name] = float(eval(expr, {"__builtins__": {}}, dict(consts)))
+    return consts
+
+
+def algorithmic_flops(c, counts, prim_kinds, pixels, scatter="Lambert"):
+    """f32 operations of one render of an in-order-loop scene (flops.h's formula).
+    counts: segments / hits / scatters / samples; prim_kinds: kind name -> count. The
+    winner-kind and scatter-class terms use the scene's single kind and class (scene_08:
+    boxes, lambertian)."""
+    seg = c["kFlopSegment"] + (c["kFlopSegmentSphere"] if prim_kinds.get("Sphere") else 0.0)
+    seg += sum(n * c[f"kFlopTest{k}"] for k, n in prim_kinds.items())
+    (kind,) = [k for k, n in prim_kinds.items() if n]
+    return (counts["segments"] * seg + counts["hits"] * c[f"kFlopHit{kind}"]
+            + counts["scatters"] * (c[f"kFlopScatter{scatter}"] + c["kFlopUnwind"])
+            + (counts["segments"] - counts["hits"]) * c["kFlopSky"]
+            + counts["samples"] * (c["kFlopCamera"] + c["kFlopSum"]) + pixels * c["kFlopPixel"])
+
+
 def algorithmic_bytes(n_pixels, n_prims):
-    """Compulsory HBM bytes of one render, charged to the trace kernel
-    that does the work: the scene read once (64 B geometry record + 16 B attenuation +
-    16 B material + 4 B scatter class = 100 B per primitive) and each pixel's result
-    written once (12 B f32 mean + 3 B u8). The per-sample colour buffer between the
-    trace and sum kernels is a design cost, not algorithmic; its bytes show in
-    `traffic` (PMC)."""
+    """Compulsory HBM bytes of one render: the scene read once (64 B
+    geometry record + 16 B attenuation + 16 B material + 4 B scatter class = 100 B per
+    primitive) and each pixel's result written once (12 B f32 mean + 3 B u8)."""
     return n_prims * 100 + n_pixels * 15
 
 
-def algorithmic_flops(segments, hits, samples, n_prims):
-    """Lower bound of the f32 arithmetic of an all-box scene: per segment
-    3 divides (1/d) + 12 per box slab test; per hit 6 (hit point); per sample 24
-    (jitter + camera ray)."""
-    return segments * (3 + 12 * n_prims) + hits * 6 + samples * 24
+# ---- in-run hardware counters (rocprofv3, child process) ----------------------
 
+PMC_PASSES = (
+    ("sq", ["SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]),
+    ("fetch", ["FETCH_SIZE"]),
+    ("write", ["WRITE_SIZE"]),
+)
+
+
+def _run_killable(cmd, timeout, env, log):
+    with open(log, "w") as f:
+        p = subprocess.Popen(cmd, stdout=f, stderr=subprocess.STDOUT, env=env, start_new_session=True)
+        try:
+            return p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return -9
+
+
+def pmc_in_run(frames=2, timeout=150):
+    """Per-launch counters of trace_kernel for this workload: one rocprofv3 pass per
+    counter group (never combined with other traces), each with --kernel-trace --stats
+    for that pass's own launch durations. Returns a dict, or {"error": ...}."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return {"error": "rocprofv3 not found"}
+    out = tempfile.mkdtemp(prefix="fr_pmc_")
+    env = dict(os.environ, FR_NO_TORCH="1", TMPDIR="/tmp")
+    prog = [sys.executable, os.path.join(ROOT, "tools", "pmc_frame.py"), SCENE, str(WIDTH), str(HEIGHT), str(SPP),
+            str(DEPTH), str(frames)]
+    res = {}
+    for tag, counters in PMC_PASSES:
+        d = os.path.join(out, tag)
+        rc = _run_killable([exe, "--pmc", *counters, "--kernel-trace", "--stats", "-d", d, "-o", tag,
+                            "--output-format", "csv", "--", *prog], timeout, env, d + ".log")
+        if rc != 0:
+            return {"error": f"rocprofv3 pass {tag} exited {rc}", "log": open(d + ".log").read()[-800:]}
+        vals = {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            import csv
+            for r in csv.DictReader(open(f)):
+                if "trace_kernel" in r["Kernel_Name"]:
+                    vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
+            import csv
+            for r in csv.DictReader(open(f)):
+                if "trace_kernel" in r["Name"]:
+                    res[f"{tag}_avg_ns"] = float(r["AverageNs"])
+        for k, v in vals.items():
+            res[k] = sum(v) / len(v)
+    keep = os.environ.get("FR_BENCH_PMC_DIR")
+    if keep:
+        shutil.copytree(out, keep, dirs_exist_ok=True)
+    shutil.rmtree(out, ignore_errors=True)
+    return res
+
+
+def valu_issue(pmc):
+    """SQ_INSTS_VALU (wave instructions per launch) against the chip's issue rate over the
+    profiled launch: 1024 SIMDs x clock / 2 cycles, the clock from GRBM_GUI_ACTIVE (summed
+    over the 8 XCDs) over the same launch's duration."""
+    ns = pmc.get("sq_avg_ns")
+    if not ns or "SQ_INSTS_VALU" not in pmc or "GRBM_GUI_ACTIVE" not in pmc:
+        return None
+    clk = pmc["GRBM_GUI_ACTIVE"] / 8 / (ns * 1e-9)
+    peak = N_SIMDS * clk / 2
+    return {"insts_per_launch": pmc["SQ_INSTS_VALU"], "launch_ns": ns, "clock_ghz": round(clk / 1e9, 3),
+            "frac": round(pmc["SQ_INSTS_VALU"] / (ns * 1e-9) / peak, 4),
+            "source": "rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-trace in this run"}
+
+
+def hbm_traffic(pmc):
+    """HBM bytes per trace launch: 2 x FETCH_SIZE (gfx950 tallies a 128-B read at 64 B,
+    MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both in KB, separate passes."""
+    if "FETCH_SIZE" not in pmc or "WRITE_SIZE" not in pmc:
+        return None
+    return (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
+
+
+# ---- CPU baseline ----------------------------------------------------------------
+
+def host_info():
+    info = {"nproc": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        info["cgroup_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        info["cgroup_cpus"] = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return info
+
+
+def cpu_baseline(budget_s=12.0):
+    """The oracle (oracle/oracle.cpp, a C++ restatement of tracer.rs's save_image) on
+    this host, over a bounded row sample of the same workload: `cpu-omp` on every core
+    this process may run on (rows and 32-pixel chunks over threads, the render_mt
+    shape), and `cpu-ref` on one thread (the save_image shape)."""
+    from oracle import oracle_py, scene_ref
+    import forma_rt as fr
+
+    host = host_info()
+    threads = max(1, host["affinity"])
+    prims, (frm, at, vup, fov) = scene_ref.load_json(open(fr.scene_path(SCENE)).read())
+    cam = oracle_py.camera_look(frm, at, vup, fov, 0.1, WIDTH, HEIGHT)
+
+    def timed(step, nthreads, col_step=1):
+        t = time.perf_counter()
+        _, _, cnt, rows = oracle_py.render(prims, cam, WIDTH, HEIGHT, SPP, DEPTH, SEED, row_step=step,
+                                           threads=nthreads, col_step=col_step)
+        return cnt, rows, time.perf_counter() - t
+
+    # calibrate on 8 spread rows, about two 32-pixel chunks per thread, then size the
+    # sample to the budget
+    cnt, rows, dt = timed(HEIGHT // 8, threads, col_step=max(1, 8 * WIDTH // (64 * threads)))
+    per_sample = dt / max(1, cnt["samples"])
+    want_rows = max(1, int(budget_s / per_sample / (WIDTH * SPP)))
+    step = max(1, HEIGHT // want_rows)
+    cnt, rows, dt = timed(step, threads)
+    if dt < 0.5 * budget_s and step > 1:  # the calibration overstated the cost: widen once
+        step = max(1, int(step * dt / budget_s))
+        cnt, rows, dt = timed(step, threads)
+    omp = {"value": round(cnt["samples"] / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": f"{rows} of {HEIGHT} rows (every {step}th) of {SCENE} {WIDTH}x{HEIGHT} {SPP}spp depth {DEPTH}, "
+                     f"{cnt['samples']} samples in {dt:.2f}s on {threads} threads, oracle/oracle.cpp (-O2)",
+           "segments_per_sample": round(cnt["segments"] / max(1, cnt["samples"]), 4), "host": host}
+    # one thread: the same rows, every cstep-th pixel of them, sized to a third of the budget
+    # assuming at most linear scaling (a thread is at least 1/threads of the whole)
+    cstep = max(1, int(threads * 3))
+    cnt1, rows1, dt1 = timed(step, 1, col_step=cstep)
+    omp["single_thread"] = {"value": round(cnt1["samples"] / dt1 / 1e6, 4), "unit": "Msamples/s", "cores": 1,
+                            "kind": "port", "sample": f"the same {rows1} rows, every {cstep}th pixel: "
+                                                      f"{cnt1['samples']} samples in {dt1:.2f}s "
+                                                      "(cpu-ref, the save_image shape)"}
+    return omp
+
+
+# ---- the run --------------------------------------------------------------------
 
 class Barrier:
     def __init__(self, world):
@@ -93,65 +270,38 @@ class Barrier:
         if self.world > 1:
             self.dist.barrier()
 
-    def max(self, v):
+    def reduce(self, v, op):
         if self.world == 1:
             return v
         import torch
         t = torch.tensor([float(v)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=op)
         return float(t.item())
+
+    def max(self, v):
+        return v if self.world == 1 else self.reduce(v, self.dist.ReduceOp.MAX)
 
     def sum(self, v):
-        if self.world == 1:
-            return v
-        import torch
-        t = torch.tensor([float(v)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return v if self.world == 1 else self.reduce(v, self.dist.ReduceOp.SUM)
 
 
-def device_sync():
-    try:
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-    except Exception:
-        pass
+def device_sync(ctx):
+    """Every stream of the render context, then the whole device."""
+    import torch
+    ctx.wait()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
 
 
-def run_gpu_steps(fr, ctx, scene, cam, params, steps, sync_all):
-    """Render `steps` frames (this rank's shard); returns per-step stats."""
+def run_steps(ctx, scene, cam, params, frame, steps):
+    """Render `steps` frames of this rank's shard, each followed by its asynchronous gather
+    into the pinned host frame; returns per-step stats."""
     stats = []
     for _ in range(steps):
         ctx.render(scene, cam, params)
         stats.append(ctx.sync())
+        ctx.download_async(frame)
     return stats
-
-
-def cpu_baseline(budget_s=12.0):
-    """The oracle (oracle/oracle.cpp, a C++ restatement of tracer.rs's save_image) on
-    this host's cores, over a bounded row sample of the same workload."""
-    from oracle import oracle_py, scene_ref
-    import forma_rt as fr
-
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-    prims, (frm, at, vup, fov) = scene_ref.load_json(open(fr.scene_path(SCENE)).read())
-    cam = oracle_py.camera_look(frm, at, vup, fov, 0.1, WIDTH, HEIGHT)
-    # calibrate on two rows per thread (every thread busy), then size the sample to ~budget_s
-    step = max(1, HEIGHT // (2 * threads))
-    t = time.perf_counter()
-    _, _, cnt, rows = oracle_py.render(prims, cam, WIDTH, HEIGHT, SPP, DEPTH, SEED, row_step=step, threads=threads)
-    dt = time.perf_counter() - t
-    per_row = dt / max(1, rows)  # wall time per row with all threads working
-    want_rows = max(threads, int(budget_s / max(per_row, 1e-6)))
-    step = max(1, HEIGHT // want_rows)
-    t = time.perf_counter()
-    _, _, cnt, rows = oracle_py.render(prims, cam, WIDTH, HEIGHT, SPP, DEPTH, SEED, row_step=step, threads=threads)
-    dt = time.perf_counter() - t
-    return {"value": round(cnt["samples"] / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{rows} of {HEIGHT} rows (every {step}th) of {SCENE} {WIDTH}x{HEIGHT} {SPP}spp depth {DEPTH}, "
-                      f"{cnt['samples']} samples in {dt:.2f}s, {threads} threads, oracle/oracle.cpp (-O2)",
-            "segments_per_sample": round(cnt["segments"] / max(1, cnt["samples"]), 4)}
 
 
 def main():
@@ -160,78 +310,79 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--verify", action="store_true", help="gather the frame on rank 0 and report a checksum")
+    ap.add_argument("--verify", action="store_true", help="stitch the frame on rank 0 and report a checksum")
     a = ap.parse_args()
 
     rank, world, local = dist_env()
     # rehearsal only: run every rank on one device (timing is then meaningless)
     if os.environ.get("FR_BENCH_DEVICE") is not None:
         local = int(os.environ["FR_BENCH_DEVICE"])
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    import forma_rt as fr  # imports torch first, so one HIP runtime serves both
+    if world == 1 and a.gpus > 1:
+        sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    import torch
 
-    try:
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.set_device(local)
-    except Exception:
-        pass
+    import forma_rt as fr  # after torch, so one HIP runtime serves both
+
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
     barrier = Barrier(world)
     scene = fr.Scene.from_file(fr.scene_path(SCENE), WIDTH, HEIGHT)
     cam = scene.camera
     n_prims = len(scene)
+    kinds = {}
+    for p in scene.prims():
+        name = {fr.FR_SPHERE: "Sphere", fr.FR_PLANE: "Plane", fr.FR_AABB: "Box", fr.FR_OBB: "Obb",
+                fr.FR_TRIANGLE: "Triangle"}.get(p.kind)
+        if name:
+            kinds[name] = kinds.get(name, 0) + 1
     params = fr.make_params(WIDTH, HEIGHT, SPP, DEPTH, SEED, shard_index=rank, shard_count=world)
     ctx = fr.RenderContext(local)
+    frame = fr.PinnedFrame(WIDTH, HEIGHT)
 
-    run_gpu_steps(fr, ctx, scene, cam, params, a.warmup, device_sync)
+    run_steps(ctx, scene, cam, params, frame, a.warmup)
+    device_sync(ctx)
     barrier()
-    device_sync()
+    device_sync(ctx)
     t0 = time.perf_counter()
-    stats = run_gpu_steps(fr, ctx, scene, cam, params, a.steps, device_sync)
-    device_sync()
+    stats = run_steps(ctx, scene, cam, params, frame, a.steps)
+    device_sync(ctx)  # the last frame's gather has landed
     t1 = time.perf_counter()
     barrier()
     elapsed = barrier.max(t1 - t0)
 
+    n = max(1, len(stats))
     my_samples = sum(s["samples"] for s in stats)
     total_samples = barrier.sum(my_samples)
-    segs = sum(s["segments"] for s in stats)
-    hits = sum(s["hits"] for s in stats)
-    kernel_ms = sum(s["kernel_ms"] for s in stats) / max(1, len(stats))
-    trace_ms = sum(s["trace_ms"] for s in stats) / max(1, len(stats))  # trace_kernel launches of one frame
-    launches = max(1, stats[0]["trace_launches"])                       # sample-block passes
-    launch_ms = trace_ms / launches                                       # what rocprof's average reports
+    counts = {k: sum(s[k] for s in stats) / n for k in ("segments", "hits", "scatters", "samples")}
+    kernel_ms = sum(s["kernel_ms"] for s in stats) / n        # the render on its streams (trace + sum)
+    trace_ms = sum(s["trace_ms"] for s in stats) / n          # trace_kernel launches of one frame
+    launches = max(1, stats[0]["trace_launches"])              # sample-block passes
+    launch_ms = trace_ms / launches                            # what rocprof's average reports
     kernel_ms_max = barrier.max(kernel_ms)
-    total_segs = barrier.sum(segs)
+    render_only = barrier.sum(my_samples / n) / (kernel_ms_max * 1e-3) / 1e6
+    total_segs = barrier.sum(counts["segments"] * n)
 
-    # roofline of the dominant kernel (trace_kernel), per launch on this rank
+    # rooflines of the dominant kernel (trace_kernel), per launch on this rank
     pixels = len(shard_rows(HEIGHT, rank, world)) * WIDTH
-    # a launch renders 1/launches of the frame's samples: its share of the frame's bytes
-    bytes_launch = algorithmic_bytes(pixels, n_prims) / launches
-    achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(PMC_FILE):
-        try:
-            pm = json.load(open(PMC_FILE))
-            if pm.get("workload") == f"{SCENE} {WIDTH}x{HEIGHT} {SPP}spp d{DEPTH}" and world == 1:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    flops_launch = algorithmic_flops(segs / len(stats), hits / len(stats), my_samples / len(stats), n_prims) / launches
+    c = flop_constants()
+    flops_launch = algorithmic_flops(c, counts, kinds, pixels) / launches
     tflops = flops_launch / (launch_ms * 1e-3) / 1e12
+    bytes_launch = algorithmic_bytes(pixels, n_prims) / launches
+    gbs = bytes_launch / (launch_ms * 1e-3) / 1e9
 
     checksum = None
     if a.verify:
-        mean, _ = ctx.download(WIDTH, HEIGHT)
-        frame = gather_frame(mean, rank, world, HEIGHT)
+        frame_img = gather_frame(frame.mean, rank, world, HEIGHT)
         if rank == 0:
             import hashlib
-            checksum = hashlib.sha256(frame.tobytes()).hexdigest()[:16]
+            checksum = hashlib.sha256(frame_img.tobytes()).hexdigest()[:16]
     if rank != 0:
         return
+    pmc = pmc_in_run() if (world == 1 and not a.no_pmc) else {}
+    issue = valu_issue(pmc)
+    traffic = hbm_traffic(pmc)
     value = total_samples / elapsed / 1e6
     out = {
         "metric": "Msamples/sec (pixels×spp) at 1920×1080, 256 spp, 8 bounces; 1/2/4/8 GPU",
@@ -249,24 +400,34 @@ def main():
         "config": {"workload": f"{SCENE} {WIDTH}x{HEIGHT} {SPP}spp {DEPTH} bounces (BASELINE config 3)",
                    "scene": SCENE, "width": WIDTH, "height": HEIGHT, "spp": SPP, "max_depth": DEPTH, "seed": SEED,
                    "parallelism": f"row-strips x{world}"},
+        "step": "render of the rank's strips + D2H gather of its f32 means and u8 image into pinned host memory",
+        "render_only_value": round(render_only, 3),
+        "render_only_ms_per_step": round(kernel_ms_max, 3),
         "segments_per_sample": round(total_segs / max(1.0, total_samples), 4),
-        "kernel_ms": round(kernel_ms, 3),
+        "scatters_per_sample": round(counts["scatters"] / max(1.0, counts["samples"]), 4),
         "trace_kernel_ms": round(trace_ms, 3),
         "trace_launches": launches,
         "trace_kernel_ms_per_launch": round(launch_ms, 3),
-        "kernel_ms_max_rank": round(kernel_ms_max, 3),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 8), "traffic": traffic,
-                     "kernel": "trace_kernel", "bytes_per_launch": round(bytes_launch)},
-        "valu_roofline": {"bound": "valu", "achieved": round(tflops, 3), "peak": FP32_PEAK_TFLOPS,
-                          "unit": "TFLOP/s", "frac": round(tflops / FP32_PEAK_TFLOPS, 5),
-                          "flops_per_launch": int(flops_launch), "note": "algorithmic lower bound, DESIGN.md §5"},
+        "occupancy_wg_per_cu": stats[0]["occupancy"],
+        "roofline": {"bound": "valu", "achieved": round(tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tflops / FP32_PEAK_TFLOPS, 5), "traffic": round(traffic) if traffic else None,
+                     "kernel": "trace_kernel", "flops_per_launch": round(flops_launch),
+                     "flop_model": "fo-rma_amd/csrc/flops.h x exact counters", "valu_issue": issue},
+        "hbm_roofline": {"bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 8), "bytes_per_launch": round(bytes_launch),
+                         "traffic": round(traffic) if traffic else None,
+                         "measured_gbs": round(traffic / (launch_ms * 1e-3) / 1e9, 2) if traffic else None},
     }
+    if pmc:
+        out["pmc"] = pmc
     if checksum:
         out["frame_sha256_16"] = checksum
     if world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_budget)
+        out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
     print(json.dumps(out), flush=True)
+    frame.close()
+    ctx.close()
 
 
 if __name__ == "__main__":

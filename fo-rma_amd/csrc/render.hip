@@ -76,7 +76,7 @@ constexpr uint32_t kBatch = 64;
 static_assert(sizeof(fr_prim) == 88, "fr_prim layout");
 static_assert(sizeof(fr_camera) == 104, "fr_camera layout");
 static_assert(sizeof(fr_params) == 40, "fr_params layout");
-static_assert(sizeof(fr_stats) == 64, "fr_stats layout");
+static_assert(sizeof(fr_stats) == 72, "fr_stats layout");
 
 struct DeviceCopy {
   int device = -1;
@@ -108,6 +108,7 @@ struct KScene {
   uint32_t n;
   uint32_t n_segs;                  // segment count (0: no BVH)
   uint32_t att_nonneg;              // every attenuation component finite and >= +0
+  float reach;                      // BVH node cull is conservative for max|o_k| <= reach (bvh.h)
 };
 
 struct KParams {
@@ -122,6 +123,7 @@ struct KParams {
   uint32_t row_magic, row_shift;      // x / tiles_per_row = fastdiv(x, row_magic, row_shift)
   uint32_t band_h;                    // FR_FLAG_MT_BANDS: rows per band, H / 4 (tracer.rs:87)
   uint32_t prio_at[3];  // a wave reserving a batch at or past prio_at[k] raises its priority to k + 1
+  uint32_t ks;          // sample slots per work item in the sample buffer: min(spp, kBlockSamples)
 };
 
 // Unsigned 32-bit division by the invariant n_tiles: q = (t + ((x - t) >> s1)) >> s2 with
@@ -146,8 +148,10 @@ static void fastdiv_magic(uint32_t d, uint32_t& m, uint32_t& shifts) {
 // Work buffers of one render pass.
 struct KWork {
   uint32_t* queue;            // next unclaimed item (zeroed before the pass)
-  float* samples;             // per-sample colours, [(s - 16*b0) * P + q] x 3 f32
-  unsigned long long* counters;
+  // per-sample colours, item-major: sample s of item (b, q) at [(item * ks + s - 16 b)] x 3 f32,
+  // item = (b - b0) * P + q, so one item's samples are contiguous (192 B at ks = 16)
+  float* samples;
+  unsigned long long* counters;  // [0] segments, [1] hits, [2] scatters
 };
 
 // camera.rs fields the ray generator reads: position, lower_left_corner,
@@ -207,6 +211,11 @@ __device__ __forceinline__ uint32_t buf_load1(const void* base, uint32_t byte_of
 
 constexpr uint32_t kAttLds = 1024;  // attenuation/class entries staged in LDS (16 B each)
 constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for small scenes
+// Sample colours a lane stages in LDS before storing them to the (item-major) sample
+// buffer: 4 x 12 B = three 16-B stores per 4 samples instead of four scattered 12-B
+// stores, which L2 wrote back as partial lines (3.5x WRITE_SIZE). The BVH kernels keep
+// their LDS for the traversal stack (occupancy) and store each sample directly.
+__host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? 1u : 4u; }
 
 // FR_DIAG builds count, per phase, wave-level trips (one per SIMT pass of the wave)
 // and lane-level work, to measure SIMT efficiency. Never enabled in the product.
@@ -317,11 +326,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   //      [stack: MAXD ? kBlock x MAXD u16 (lane-major) : max_depth x kBlock u32]
   // Entry n of the attenuations is (1, 1, 1): the depth-8 stack's empty levels hold n.
   // Staging the winner's data keeps per-lane global gathers off the shading path.
+  // [STG > 1: kBlock x STG staged sample colours (12 B each), lane-major] in front.
   extern __shared__ uint32_t lds[];
+  constexpr uint32_t STG = stage_samples(BVH);
+  float* stage = reinterpret_cast<float*>(lds) + threadIdx.x * (3u * STG);
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
   const uint32_t n_att_st = n_att ? n_att + 1u : 0u;  // with the unit entry
   const uint32_t n_rec = sc.n <= kRecLds ? sc.n : 0u;
-  float4* att_lds = reinterpret_cast<float4*>(lds);
+  float4* att_lds = reinterpret_cast<float4*>(lds + (STG > 1 ? kBlock * 3u * STG : 0u));
   float4* rec_lds = att_lds + n_att_st;
   uint32_t* stack = reinterpret_cast<uint32_t*>(rec_lds + 4u * n_rec);
   uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
@@ -351,7 +363,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 
 
   const float fW = static_cast<float>(kp.W), fH = static_cast<float>(kp.H);
-  const uint32_t s_pass = kp.b0 * kBlockSamples;
 
   enum : uint32_t { NEED_NONE = 0, NEED_LENS = 1, NEED_SPHERE = 2 };
   uint32_t depth = 0;
@@ -369,9 +380,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   V3 sn{0.0f, 0.0f, 0.0f};  // metal: normal
   float sfuzz = 0.0f, fx = 0.0f, fy = 0.0f, vofs = 0.0f;
   bool smetal = false;
-  uint32_t sbest = 0, q = 0, s = 0, s_end = 0, nseg = 0, nhit = 0;
-  float* out = kw.samples;                               // colour slot of the current sample
-  const size_t out_stride = 3 * static_cast<size_t>(kp.P);  // next sample of the same pixel
+  uint32_t sbest = 0, q = 0, s = 0, s_end = 0, nseg = 0, nhit = 0, nscat = 0;
+  uint32_t jj = 0;           // sample index within the item's block
+  float* out = kw.samples;   // the item's first sample slot (item-major buffer)
   Rng rng{0u, 0u, 0u, 0u};
   bool active = true, need_item = true, need_jit = false, have_ray = false;
   uint32_t need = NEED_NONE;
@@ -454,7 +465,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         if (ok) {
           rng = st;  // this block's stream: rng_seed(seed, y * W + x, b)
           s = b * kBlockSamples;
-          out = kw.samples + 3 * (static_cast<size_t>(s - s_pass) * kp.P + q);
+          out = kw.samples + 3 * (static_cast<size_t>(item) * kp.ks);
+          jj = 0;
           s_end = min(s + kBlockSamples, kp.spp);
           fx = static_cast<float>(x);
           fy = static_cast<float>(yrow);
@@ -529,6 +541,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           if (ok) {
             push(sbest);
             ++depth;
+            ++nscat;
             d = dir;
             have_ray = true;
           } else {
@@ -548,7 +561,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       const float a_dd = dot(d, d);
       float closest = FLT_MAX, t_last = 0.0f;
       int best = -1;
+      // The node cull is conservative only for origins within kBvhOriginReach scene
+      // extents (bvh.h). A stale plane record (plane.rs:27-40) can put a scatter origin
+      // p = o + t_stale d far outside: a wave holding such a lane (or a NaN origin) tests
+      // the list in order instead, which the BVH walk equals bit for bit.
+      bool list_walk = !BVH;
       if (BVH) {
+        const float ao = fmax3_num(__builtin_fabsf(o.x), __builtin_fabsf(o.y), __builtin_fabsf(o.z));
+        list_walk = __ballot(!(ao <= sc.reach)) != 0;
+      }
+      if (BVH && !list_walk) {
         // The list cut at its planes (bvh.h), walked in list order: each plane tested
         // where it stands, each run of other primitives through its own tree. A
         // primitive's candidate t does not depend on t_max, so a run's effect is the
@@ -646,7 +668,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           }
         }
       }
-      for (uint32_t ii = 0; ii < (BVH ? 0u : sc.n); ++ii) {
+      for (uint32_t ii = 0; ii < (list_walk ? sc.n : 0u); ++ii) {
         // the index is wave-uniform; say so, or the compiler may fall back to vector loads
         const uint32_t i = __builtin_amdgcn_readfirstlane(ii);
         const RecRef r4 = rec_at(sc.rec, i);  // scalar loads
@@ -730,6 +752,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
             const V3 nd = scatter_dielectric(d, n, rng);
             push(static_cast<uint32_t>(best));
             ++depth;
+            ++nscat;
             o = p;
             d = nd;
             have_ray = true;
@@ -792,10 +815,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           for (int j = udepth - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
         }
       }
-      out[0] = col.x;
-      out[1] = col.y;
-      out[2] = col.z;
-      out += out_stride;
+      if (STG == 1) {
+        out[3 * jj] = col.x;
+        out[3 * jj + 1] = col.y;
+        out[3 * jj + 2] = col.z;
+      } else {
+        // stage the colour; every STG-th sample of the block, and its last, go out together
+        float* sl = stage + 3u * (jj & (STG - 1u));
+        sl[0] = col.x;
+        sl[1] = col.y;
+        sl[2] = col.z;
+        const bool full = (jj & (STG - 1u)) == STG - 1u;
+        if (full || s + 1u == s_end) {
+          float* dst = out + 3u * (jj & ~(STG - 1u));
+          if (full && kp.ks == kBlockSamples) {
+            // 16-B aligned: item * 192 B + a multiple of 48 B
+            const float4* src = reinterpret_cast<const float4*>(stage);
+#pragma unroll
+            for (uint32_t k = 0; k < 3u * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
+          } else {
+            for (uint32_t k = 0; k < 3u * ((jj & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
+          }
+        }
+      }
+      ++jj;
       if (++s == s_end)
         need_item = true;
       else
@@ -805,14 +848,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   }
 
   // per-wave counter reduction, one 64-bit atomic per wave per counter
-  unsigned long long a = nseg, b = nhit;
+  unsigned long long a = nseg, b = nhit, sct = nscat;
   for (int m = 32; m > 0; m >>= 1) {
     a += __shfl_xor(a, m);
     b += __shfl_xor(b, m);
+    sct += __shfl_xor(sct, m);
   }
   if (lane == 0 && (a | b)) {
     atomicAdd(&kw.counters[0], a);
     atomicAdd(&kw.counters[1], b);
+    atomicAdd(&kw.counters[2], sct);
   }
 #ifdef FR_PROF
   if (lane == 0)
@@ -847,16 +892,19 @@ __global__ __launch_bounds__(256) void sum_kernel(KParams kp, const float* __res
     return;
   }
   V3 sum = first ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
-  const uint32_t s0 = kp.b0 * kBlockSamples;
-  const uint32_t s1 = min((kp.b0 + kp.nb) * kBlockSamples, kp.spp);
   const float fspp = static_cast<float>(kp.spp);
-  for (uint32_t s = s0; s < s1; ++s) {
-    const float* c = samples + 3 * (static_cast<size_t>(s - s0) * kp.P + q);
-    if (mt)  // save_image_mt (tracer.rs:140-145): acc += (sqrt(c) * 255) as u8 / sample
-      sum = add(sum, V3{static_cast<float>(to_u8(c[0])) / fspp, static_cast<float>(to_u8(c[1])) / fspp,
-                        static_cast<float>(to_u8(c[2])) / fspp});
-    else
-      sum = add(sum, V3{c[0], c[1], c[2]});
+  for (uint32_t bl = 0; bl < kp.nb; ++bl) {
+    // the item's samples are contiguous (item-major buffer, KWork::samples)
+    const uint32_t s0 = (kp.b0 + bl) * kBlockSamples;
+    const uint32_t n = min(kBlockSamples, kp.spp - s0);
+    const float* c = samples + 3 * (static_cast<size_t>(bl * kp.P + q) * kp.ks);
+    for (uint32_t j = 0; j < n; ++j, c += 3) {
+      if (mt)  // save_image_mt (tracer.rs:140-145): acc += (sqrt(c) * 255) as u8 / sample
+        sum = add(sum, V3{static_cast<float>(to_u8(c[0])) / fspp, static_cast<float>(to_u8(c[1])) / fspp,
+                          static_cast<float>(to_u8(c[2])) / fspp});
+      else
+        sum = add(sum, V3{c[0], c[1], c[2]});
+    }
   }
   if (!last) {
     running[3 * q] = sum.x;
@@ -1104,7 +1152,14 @@ struct fr_ctx {
   // Pass pipeline: traces alternate between `stream` and `stream2`,
   // sums run on `stream_sum`, so a pass's sum and tail overlap the next pass's trace.
   hipStream_t stream2 = nullptr, stream_sum = nullptr;
+  // fr_ctx_download_async: D2H copies of the last render on their own stream; the next
+  // render's first sum kernel (the first writer of d_mean / d_u8) waits for ev_copy, so a
+  // frame's gather overlaps the next frame's trace.
+  hipStream_t stream_copy = nullptr;
+  hipEvent_t ev_copy = nullptr;
+  bool copy_pending = false;
   int passes = 0;
+  int occupancy = 0;  // trace-kernel workgroups per CU of the last launch (occupancy API)
   float* d_mean = nullptr;
   uint8_t* d_u8 = nullptr;
   unsigned long long* d_cnt = nullptr;  // [0..3] counters, [4..] diagnostics; [31] queue head
@@ -1121,19 +1176,39 @@ struct fr_ctx {
 // Picks the specialisation: single-kind scenes (all boxes, all spheres) drop the
 // per-primitive kind switch; HAS_PLANE adds the stale-record bookkeeping; small depth
 // uses the u16 stack with the unrolled unwind.
+// Persistent grid: as many workgroups as are resident at once (the occupancy API reads the
+// kernel's registers and this launch's LDS), or fewer for a small pass. A workgroup
+// beyond the resident count would start only after the queue has drained.
+struct Grid {
+  uint64_t want;  // workgroups the pass could use (items / kBlock)
+  int num_cus;
+  int* per_cu;    // out: resident workgroups per CU
+};
+
+template <typename Kern>
+static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t st, const KArgs& a) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, static_cast<int>(kBlock), lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  *g.per_cu = per_cu;
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * static_cast<uint64_t>(g.num_cus);
+  const uint32_t blocks = static_cast<uint32_t>(g.want < cap ? (g.want ? g.want : 1u) : cap);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, st, a);
+}
+
 template <int KS, bool HP, bool BV, bool MT = false>
-static void launch_depth(bool small_depth, dim3 g, size_t lds, hipStream_t st, const KScene& ks, const KCam& kc,
-                         const KParams& kp, const KWork& kw) {
+static void launch_depth(bool small_depth, const Grid& g, size_t lds, hipStream_t st, const KScene& ks,
+                         const KCam& kc, const KParams& kp, const KWork& kw) {
   if (small_depth)
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV, MT>), g, dim3(kBlock), lds, st,
-                       KArgs{ks, kc, kp, kw});
+    launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV, MT>, g, lds, st, KArgs{ks, kc, kp, kw});
   else
-    hipLaunchKernelGGL((trace_kernel<KS, HP, FR_KREJ, 0, BV, MT>), g, dim3(kBlock), lds, st, KArgs{ks, kc, kp, kw});
+    launch_persistent(trace_kernel<KS, HP, FR_KREJ, 0, BV, MT>, g, lds, st, KArgs{ks, kc, kp, kw});
 }
 
 // BVH kernels walk the list's segments (bvh.h); scenes with planes use the general
 // kernel, which tests each plane in list order between the runs.
-static void launch_trace(uint32_t kinds, bool has_plane, bool bvh, bool small_depth, dim3 g, size_t lds,
+static void launch_trace(uint32_t kinds, bool has_plane, bool bvh, bool small_depth, const Grid& g, size_t lds,
                          hipStream_t st, const KScene& ks, const KCam& kc, const KParams& kp, const KWork& kw) {
   if (kp.flags & FR_FLAG_MT_BANDS) {  // save_image_mt: the general kernels, in-order loop
     if (has_plane)
@@ -1220,6 +1295,8 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
       hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream_sum, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream_copy, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&c->d_cnt, 32 * sizeof(unsigned long long)) != hipSuccess) {
     fr_ctx_free(c);
     return set_error(FR_EHIP, "fr_ctx_create: event/counter allocation failed");
@@ -1232,6 +1309,8 @@ void fr_ctx_free(fr_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->stream_copy) (void)hipStreamSynchronize(c->stream_copy), (void)hipStreamDestroy(c->stream_copy);
+  if (c->ev_copy) (void)hipEventDestroy(c->ev_copy);
   if (c->d_mean) (void)hipFree(c->d_mean);
   if (c->d_u8) (void)hipFree(c->d_u8);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
@@ -1258,6 +1337,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   if (rc) return rc;
   const size_t pixels = static_cast<size_t>(p->width) * p->height;
   if (pixels > c->cap_pixels) {
+    if (c->copy_pending) HIPCHK(hipStreamSynchronize(c->stream_copy));  // a gather still reads them
     if (c->d_mean) HIPCHK(hipFree(c->d_mean));
     if (c->d_u8) HIPCHK(hipFree(c->d_u8));
     c->d_mean = nullptr;
@@ -1286,6 +1366,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   ks.lrec = reinterpret_cast<const float4*>(b + dc->off_lrec);
   ks.segs = reinterpret_cast<const uint4*>(b + dc->off_segs);
   ks.n_segs = use_bvh ? dc->n_segs : 0u;
+  ks.reach = kBvhOriginReach * (dc->bvh_extent + 1.0f);
   ks.att_nonneg = dc->att_nonneg ? 1u : 0u;
   KCam kc{cam->position[0], cam->position[1], cam->position[2], cam->lower_left[0], cam->lower_left[1],
           cam->lower_left[2], cam->horizontal[0], cam->horizontal[1], cam->horizontal[2], cam->vertical[0],
@@ -1318,7 +1399,9 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   // (FR_SAMPLE_BUFFER_GB) may force more. Two pipelined passes measured 0.6 % faster
   // on C3, but overlapping launches blur each launch's own HIP-event time (DESIGN.md
   // §4.5a), so one pass is the default.
-  const size_t per_block = static_cast<size_t>(kp.P) * kBlockSamples * 3 * sizeof(float);
+  // sample slots per item: a frame of spp < 16 (update()'s 1-spp frames) needs only spp
+  kp.ks = p->spp < kBlockSamples ? (p->spp ? p->spp : 1u) : kBlockSamples;
+  const size_t per_block = static_cast<size_t>(kp.P) * kp.ks * 3 * sizeof(float);
   // FR_TAIL_PRIO=d: priority from the last 1/d, 1/(4d), 1/(16d) of the queue (0: off)
   uint32_t tail_prio = 8;
   if (const char* e = getenv("FR_TAIL_PRIO")) tail_prio = static_cast<uint32_t>(atoi(e) > 0 ? atoi(e) : 0);
@@ -1373,8 +1456,9 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
                                          : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
                                                sizeof(uint32_t);
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
-  const size_t lds = (n_att ? n_att + 1 : 0) * 16 + n_rec * 64 + stack_bytes +
-                     (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
+  const size_t stage_n = stage_samples(use_bvh);
+  const size_t lds = (stage_n > 1 ? kBlock * stage_n * 3 * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
+                     n_rec * 64 + stack_bytes + (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
   KWork kw;
   kw.counters = c->d_cnt;
   c->t0 = std::chrono::steady_clock::now();
@@ -1406,18 +1490,18 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
       if (pass >= 2) HIPCHK(hipStreamWaitEvent(ts, c->ev_sum[pass - 2], 0));  // the slot's last reader is done
       kw.queue = reinterpret_cast<uint32_t*>(c->d_cnt + 31 - slot);
       kw.samples = samples;
-      // persistent grid: enough waves to fill every CU (extra blocks find the queue empty)
-      const uint64_t want = (static_cast<uint64_t>(kp.n_items) + 255u) / 256u;
-      const uint32_t blocks = static_cast<uint32_t>(want < 8ull * c->num_cus ? want : 8ull * c->num_cus);
+      // persistent grid: the resident workgroup count (launch_persistent)
+      const Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy};
       HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), ts));
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced], ts));
-      launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, dim3(blocks), lds, ts, ks, kc, kp, kw);
+      launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, grid, lds, ts, ks, kc, kp, kw);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced + 1], ts));
       HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_trace[2 * traced + 1], 0));
       ++traced;
     }
     const int first = pass == 0, last = pass + 1 >= passes;
+    if (first && c->copy_pending) HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_copy, 0));  // last gather done
     hipLaunchKernelGGL(sum_kernel, dim3(sum_blocks ? sum_blocks : 1u), dim3(256), 0, c->stream_sum, kp, samples,
                        c->d_running, c->d_mean, c->d_u8, first, last);
     HIPCHK(hipGetLastError());
@@ -1497,19 +1581,25 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
     }
     st->trace_ms = tms;
     st->trace_launches = static_cast<uint32_t>(c->passes);
-    st->reserved = 0;
+    st->occupancy = static_cast<uint32_t>(c->occupancy);
+    st->scatters = cnt[2];
     st->total_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t0).count();
   }
   return FR_OK;
 }
 
-int fr_ctx_download(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
-  if (!c || !c->pending) return set_error(FR_EARG, "fr_ctx_download: nothing rendered");
-  HIPCHK(hipSetDevice(c->device));
+// Enqueues the D2H copies of this shard's rows of the last render on `st`.
+static int enqueue_download(fr_ctx* c, hipStream_t st, float* mean_rgb, uint8_t* rgb8) {
   const fr_params& p = c->last;
   const uint32_t strips = (p.height + kStripRows - 1) / kStripRows;
   const size_t row_f = static_cast<size_t>(p.width) * 3;  // elements per row
+  if (p.shard_count == 1) {  // the whole image: one contiguous copy per output
+    const size_t n = static_cast<size_t>(p.height) * row_f;
+    if (mean_rgb) HIPCHK(hipMemcpyAsync(mean_rgb, c->d_mean, n * 4, hipMemcpyDeviceToHost, st));
+    if (rgb8) HIPCHK(hipMemcpyAsync(rgb8, c->d_u8, n, hipMemcpyDeviceToHost, st));
+    return FR_OK;
+  }
   // full strips of this shard form a strided 2-D region; the trailing partial strip is separate
   uint32_t full = 0, partial = 0;
   for (uint32_t k = p.shard_index; k < strips; k += p.shard_count) {
@@ -1525,25 +1615,65 @@ int fr_ctx_download(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
   if (mean_rgb) {
     if (full)
       HIPCHK(hipMemcpy2DAsync(mean_rgb + first, pitch * 4, c->d_mean + first, pitch * 4, width * 4, full,
-                              hipMemcpyDeviceToHost, c->stream));
+                              hipMemcpyDeviceToHost, st));
     if (has_partial) {
       const size_t o = static_cast<size_t>(partial) * kStripRows * row_f;
       HIPCHK(hipMemcpyAsync(mean_rgb + o, c->d_mean + o, (p.height - partial * kStripRows) * row_f * 4,
-                            hipMemcpyDeviceToHost, c->stream));
+                            hipMemcpyDeviceToHost, st));
     }
   }
   if (rgb8) {
     if (full)
-      HIPCHK(hipMemcpy2DAsync(rgb8 + first, pitch, c->d_u8 + first, pitch, width, full, hipMemcpyDeviceToHost,
-                              c->stream));
+      HIPCHK(hipMemcpy2DAsync(rgb8 + first, pitch, c->d_u8 + first, pitch, width, full, hipMemcpyDeviceToHost, st));
     if (has_partial) {
       const size_t o = static_cast<size_t>(partial) * kStripRows * row_f;
       HIPCHK(hipMemcpyAsync(rgb8 + o, c->d_u8 + o, (p.height - partial * kStripRows) * row_f,
-                            hipMemcpyDeviceToHost, c->stream));
+                            hipMemcpyDeviceToHost, st));
     }
   }
+  return FR_OK;
+}
+
+int fr_ctx_download(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
+  if (!c || !c->pending) return set_error(FR_EARG, "fr_ctx_download: nothing rendered");
+  HIPCHK(hipSetDevice(c->device));
+  const int rc = enqueue_download(c, c->stream, mean_rgb, rgb8);
+  if (rc) return rc;
   HIPCHK(hipStreamSynchronize(c->stream));
   return FR_OK;
+}
+
+int fr_ctx_download_async(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
+  if (!c || !c->pending) return set_error(FR_EARG, "fr_ctx_download_async: nothing rendered");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamWaitEvent(c->stream_copy, c->ev1, 0));  // after the last render's sum
+  const int rc = enqueue_download(c, c->stream_copy, mean_rgb, rgb8);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(c->ev_copy, c->stream_copy));
+  c->copy_pending = true;
+  return FR_OK;
+}
+
+int fr_ctx_wait(fr_ctx* c) {
+  if (!c) return set_error(FR_EARG, "fr_ctx_wait: null ctx");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream2));
+  HIPCHK(hipStreamSynchronize(c->stream_sum));
+  HIPCHK(hipStreamSynchronize(c->stream_copy));
+  return FR_OK;
+}
+
+int fr_host_alloc(size_t bytes, void** out) {
+  if (!out) return set_error(FR_EARG, "fr_host_alloc: null output");
+  *out = nullptr;
+  if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess || !*out)
+    return set_error(FR_ENOMEM, "hipHostMalloc(%zu) failed", bytes);
+  return FR_OK;
+}
+
+void fr_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 int fr_ctx_device_buffers(fr_ctx* c, float** d_mean, uint8_t** d_u8) {
@@ -1574,6 +1704,12 @@ int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* 
   if (hipGetDeviceCount(&avail) != hipSuccess || avail < n_gpus)
     return set_error(FR_ENODEV, "fr_render_hip_multi: %d devices requested, %d present", n_gpus, avail);
   // Upload on the calling thread first so the per-device threads only read the scene.
+  for (int g = 0; g < n_gpus; ++g) {
+    HIPCHK(hipSetDevice(g));
+    DeviceCopy* dc = nullptr;
+    const int rc = upload_scene(scene, g, &dc);
+    if (rc) return rc;
+  }
   std::vector<int> rcs(n_gpus, 0);
   std::vector<fr_stats> sts(n_gpus);
   std::vector<std::string> errs(n_gpus);
@@ -1601,6 +1737,8 @@ int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* 
       if (sts[g].kernel_ms > stats->kernel_ms) stats->kernel_ms = sts[g].kernel_ms;
       if (sts[g].trace_ms > stats->trace_ms) stats->trace_ms = sts[g].trace_ms;
       if (sts[g].trace_launches > stats->trace_launches) stats->trace_launches = sts[g].trace_launches;
+      stats->scatters += sts[g].scatters;
+      stats->occupancy = sts[g].occupancy;
     }
     stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }

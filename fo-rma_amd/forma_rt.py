@@ -27,7 +27,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FORMA_RT_LIB") or os.path.join(HERE, "libforma_rt.so")
 SCENES_DIR = os.path.join(HERE, "scenes")
 
-FR_ABI_VERSION = 2  # include/forma_rt.h FR_ABI_VERSION
+FR_ABI_VERSION = 3  # include/forma_rt.h FR_ABI_VERSION
 FR_OK, FR_EARG, FR_EPARSE, FR_EHIP, FR_ENODEV, FR_ENOMEM = 0, -1, -2, -3, -4, -5
 FR_SPHERE, FR_PLANE, FR_AABB, FR_OBB, FR_STUB, FR_TRIANGLE = 0, 1, 2, 3, 4, 5
 FR_LAMBERTIAN, FR_METAL, FR_DIELECTRIC, FR_LIGHT = 0, 1, 2, 3
@@ -69,7 +69,7 @@ class FrParams(C.Structure):
 class FrStats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("hits", C.c_uint64), ("samples", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("kernel_ms", C.c_double), ("total_ms", C.c_double), ("trace_ms", C.c_double),
-                ("trace_launches", C.c_uint32), ("reserved", C.c_uint32)]
+                ("trace_launches", C.c_uint32), ("occupancy", C.c_uint32), ("scatters", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -81,7 +81,8 @@ EXPORTS = (
     "fr_scene_create", "fr_scene_builtin", "fr_scene_from_json", "fr_scene_free", "fr_scene_count",
     "fr_scene_get_prims", "fr_scene_translate", "fr_scene_rotate",
     "fr_camera_init", "fr_camera_look", "fr_camera_orbit", "fr_camera_translate", "fr_update_delta",
-    "fr_ctx_create", "fr_ctx_free", "fr_ctx_render", "fr_ctx_sync", "fr_ctx_download", "fr_ctx_device_buffers",
+    "fr_ctx_create", "fr_ctx_free", "fr_ctx_render", "fr_ctx_sync", "fr_ctx_download", "fr_ctx_download_async",
+    "fr_ctx_wait", "fr_ctx_device_buffers", "fr_host_alloc", "fr_host_free",
     "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_recip",
     "fr_post_process", "fr_post_process_device", "fr_rgb_to_rgba_device",
 )
@@ -92,6 +93,9 @@ _lib = None
 def _load_torch_runtime_first():
     # If torch is importable, load it first so this library binds the same
     # libamdhip64 (soname libamdhip64.so.7) as torch: one HIP runtime per process.
+    # FR_NO_TORCH=1 skips it (a short-lived profiled child that never imports torch).
+    if os.environ.get("FR_NO_TORCH") == "1":
+        return
     try:
         import torch  # noqa: F401
     except Exception:
@@ -135,6 +139,12 @@ def lib():
     L.fr_ctx_sync.argtypes = [vp, P(FrStats)]
     L.fr_ctx_download.argtypes = [vp, f3, P(C.c_uint8)]
     L.fr_ctx_device_buffers.argtypes = [vp, P(vp), P(vp)]
+    if hasattr(L, "fr_ctx_download_async"):  # absent from A/B builds of older sources
+        L.fr_ctx_download_async.argtypes = [vp, f3, P(C.c_uint8)]
+        L.fr_ctx_wait.argtypes = [vp]
+        L.fr_host_alloc.argtypes = [C.c_size_t, P(vp)]
+        L.fr_host_free.argtypes = [vp]
+        L.fr_host_free.restype = None
     L.fr_render_hip.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
     L.fr_render_hip_multi.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
     L.fr_selftest_ops.argtypes = [C.c_int, C.c_int, f3, f3, C.c_uint32, f3]
@@ -375,6 +385,31 @@ def make_params(width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, shar
     return p
 
 
+class PinnedFrame:
+    """Full-image host buffers in page-locked memory (fr_host_alloc): mean [H, W, 3] f32
+    and u8 [H, W, 3], the targets of RenderContext.download_async."""
+
+    def __init__(self, width, height):
+        n = width * height * 3
+        self._p = C.c_void_p()
+        check(lib().fr_host_alloc(n * 5, C.byref(self._p)))
+        buf = (C.c_uint8 * (n * 5)).from_address(self._p.value)
+        self.mean = np.frombuffer(buf, dtype=np.float32, count=n).reshape(height, width, 3)
+        self.u8 = np.frombuffer(buf, dtype=np.uint8, count=n, offset=n * 4).reshape(height, width, 3)
+
+    def close(self):
+        if self._p and self._p.value:
+            self.mean = self.u8 = None
+            lib().fr_host_free(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class RenderContext:
     """One device, one HIP stream, resident output buffers (fr_ctx)."""
 
@@ -397,6 +432,17 @@ class RenderContext:
         check(lib().fr_ctx_download(self._h, mean.ctypes.data_as(C.POINTER(C.c_float)),
                                     u8.ctypes.data_as(C.POINTER(C.c_uint8))))
         return mean, u8
+
+    def download_async(self, frame):
+        """Enqueue the last render's D2H gather into `frame` (a PinnedFrame); returns at
+        once. The copies finish before wait() returns and before the next render writes
+        its outputs; the next render's trace kernel overlaps them."""
+        check(lib().fr_ctx_download_async(self._h, frame.mean.ctypes.data_as(C.POINTER(C.c_float)),
+                                          frame.u8.ctypes.data_as(C.POINTER(C.c_uint8))))
+
+    def wait(self):
+        """Block until every render and download enqueued on this context has finished."""
+        check(lib().fr_ctx_wait(self._h))
 
     def device_buffers(self):
         """(d_mean_rgb, d_rgb8) device addresses of the last render's full-image outputs."""
@@ -457,7 +503,9 @@ def post_process(rgba, effects, time=0.0, device=0):
 # ---- tracer.rs operator API ---------------------------------------------------
 
 class TraceModel:
-    """tracer.rs:12-17 {scene, width, height, pixels}"""
+    """tracer.rs:12-17 {scene, width, height, pixels}, plus the render context the frames
+    run on: one fr_ctx per model, created on the first frame and reused by every later
+    update() / save_image() (no per-frame stream, event or buffer allocation)."""
 
     def __init__(self, scene, width, height):
         self.scene, self.width, self.height = scene, width, height
@@ -465,6 +513,27 @@ class TraceModel:
         self.frame = 0
         self.seed = DEFAULT_SEED
         self.device = 0
+        self.ctx = None
+        self.last_stats = None
+
+    def context(self):
+        if self.ctx is None:
+            self.ctx = RenderContext(self.device)
+        return self.ctx
+
+    def render(self, scene, spp, max_depth, seed, mt_bands=False):
+        """One frame on the model's context: (mean[H,W,3], u8[H,W,3], stats)."""
+        ctx = self.context()
+        ctx.render(scene, self.scene.camera, make_params(self.width, self.height, spp, max_depth, seed,
+                                                         mt_bands=mt_bands))
+        self.last_stats = ctx.sync()
+        mean, u8 = ctx.download(self.width, self.height)
+        return mean, u8, self.last_stats
+
+    def close(self):
+        if self.ctx is not None:
+            self.ctx.close()
+            self.ctx = None
 
 
 def create_model(width, height, scene=None):
@@ -484,7 +553,7 @@ def update(model, keys, delta_time, max_depth=MAX_DEPTH):
     camera_orbit(model.scene.camera, list(d))
     seed = model.seed ^ (0x9E3779B97F4A7C15 * (model.frame + 1) & 0xFFFFFFFFFFFFFFFF)
     model.frame += 1
-    _, u8, _ = render(model.scene, model.scene.camera, model.width, model.height, 1, max_depth, seed, model.device)
+    _, u8, _ = model.render(model.scene, 1, max_depth, seed)
     model.pixels = u8.reshape(-1)
     return model.pixels
 
@@ -509,8 +578,7 @@ def save_image_mt(model, sample, path="out/basic_mt.png", max_depth=MAX_DEPTH):
     scene, scenes::get_simple_scene, with the model's camera), each pass gamma-corrected
     to u8, the u8 frames averaged and truncated, PNG."""
     simple = Scene.builtin(0, model.width, model.height)
-    acc, u8, stats = render(simple, model.scene.camera, model.width, model.height, sample, max_depth, model.seed,
-                            model.device, mt_bands=True)
+    acc, u8, stats = model.render(simple, sample, max_depth, model.seed, mt_bands=True)
     write_png(path, u8)
     return acc, u8, stats
 
@@ -518,7 +586,6 @@ def save_image_mt(model, sample, path="out/basic_mt.png", max_depth=MAX_DEPTH):
 def save_image(model, sample, path="out/basic.png", max_depth=MAX_DEPTH):
     """tracer.rs:160-187: `sample` spp per pixel, gamma 2, u8, PNG. Like the reference it
     fails if the output directory is missing (tracer.rs:186 unwrap)."""
-    mean, u8, stats = render(model.scene, model.scene.camera, model.width, model.height, sample, max_depth,
-                             model.seed, model.device)
+    mean, u8, stats = model.render(model.scene, sample, max_depth, model.seed)
     write_png(path, u8)
     return mean, u8, stats

@@ -45,7 +45,9 @@
 extern "C" {
 #endif
 
-#define FR_ABI_VERSION 2 /* 2: fr_stats.trace_launches; FR_TRIANGLE; post effects; FR_FLAG_MT_BANDS */
+#define FR_ABI_VERSION 3 /* 2: fr_stats.trace_launches; FR_TRIANGLE; post effects; FR_FLAG_MT_BANDS
+                            3: fr_stats.scatters/.occupancy; fr_ctx_download_async, fr_ctx_wait,
+                               fr_host_alloc/free; item-major sample buffer */
 
 /* error codes */
 #define FR_OK 0
@@ -141,7 +143,8 @@ typedef struct fr_stats {
   double total_ms;     /* host wall time of the call */
   double trace_ms;     /* HIP-event time of the trace kernel(s) alone, summed over launches */
   uint32_t trace_launches; /* trace kernel launches of the render (sample-block passes) */
-  uint32_t reserved;
+  uint32_t occupancy;  /* resident trace-kernel workgroups per CU (the persistent grid's size / CUs) */
+  uint64_t scatters;   /* successful scatters (tracer.rs:205: a segment continued by a new ray) */
 } fr_stats;
 
 typedef struct fr_scene fr_scene; /* opaque: host primitive list + per-device copies */
@@ -183,8 +186,20 @@ int fr_ctx_sync(fr_ctx* ctx, fr_stats* stats);
    (mean_rgb: W*H*3 f32, rgb8: W*H*3 u8; either may be NULL). Rows of other shards
    are left untouched. */
 int fr_ctx_download(fr_ctx* ctx, float* mean_rgb, uint8_t* rgb8);
+/* The same copies enqueued on the ctx's copy stream, after the last render; returns at
+   once. The host buffers must stay valid until fr_ctx_wait (pinned memory from
+   fr_host_alloc makes the copy asynchronous). The next fr_ctx_render's trace kernel does
+   not wait for these copies; only its writes of the output buffers do, so one frame's
+   gather overlaps the next frame's trace. */
+int fr_ctx_download_async(fr_ctx* ctx, float* mean_rgb, uint8_t* rgb8);
+/* Block until every render and download enqueued on the ctx has completed. */
+int fr_ctx_wait(fr_ctx* ctx);
 /* Device pointers of the last render's full-image output buffers. */
 int fr_ctx_device_buffers(fr_ctx* ctx, float** d_mean_rgb, uint8_t** d_rgb8);
+
+/* Page-locked host memory (hipHostMalloc) for fr_ctx_download_async targets. */
+int fr_host_alloc(size_t bytes, void** out);
+void fr_host_free(void* p);
 
 /* ---- synchronous conveniences ---- */
 /* One shard on one device; writes the shard's rows into caller-owned host buffers. */

@@ -717,13 +717,16 @@ int oracle_closest_hit(const or_prim* prims, uint32_t n, const float o[3], const
 
 // save_image's loop (tracer.rs:160-187) over the rows of one shard
 // (strips of 8 rows, strip k -> shard k % shard_count), keeping every
-// `row_step`-th of those rows (1 = all). Row-parallel over `threads`
-// (the render_mt shape, tracer.rs:83-134, without its per-pixel scene rebuild).
-// Writes means and u8 for the rows it renders; returns the number of rows.
+// `row_step`-th of those rows (1 = all) and in them every `col_step`-th pixel
+// (1 = all). Parallel over `threads` in chunks of 32 pixels of a row (the render_mt
+// shape, tracer.rs:83-134, without its per-pixel scene rebuild). Writes means and u8
+// for the pixels it renders; returns the number of rows.
 int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, uint32_t width, uint32_t height,
                       uint32_t spp, uint32_t max_depth, uint64_t seed, uint32_t shard_index, uint32_t shard_count,
-                      uint32_t row_step, int threads, float* out_mean, uint8_t* out_u8, or_counters* counters) {
-  if (!cam || width == 0 || height == 0 || shard_count == 0 || shard_index >= shard_count || row_step == 0)
+                      uint32_t row_step, uint32_t col_step, int threads, float* out_mean, uint8_t* out_u8,
+                      or_counters* counters) {
+  if (!cam || width == 0 || height == 0 || shard_count == 0 || shard_index >= shard_count || row_step == 0 ||
+      col_step == 0)
     return -1;
   const auto objects = build(prims, n);
   Camera camera;
@@ -734,14 +737,18 @@ int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, ui
     if ((y / 8) % shard_count != shard_index) continue;
     if (kept++ % row_step == 0) rows.push_back(y);
   }
+  const uint32_t cols = (width + col_step - 1) / col_step;  // pixels x = 0, col_step, ...
+  const uint32_t chunk = 32, chunks = (cols + chunk - 1) / chunk;
   if (threads < 1) threads = 1;
   std::atomic<size_t> next{0};
   std::vector<Counters> cnts(threads);
   auto work = [&](int tid) {
     Counters& cnt = cnts[tid];
-    for (size_t ri; (ri = next.fetch_add(1)) < rows.size();) {
-      const uint32_t y = rows[ri];
-      for (uint32_t x = 0; x < width; ++x) {
+    for (size_t wi; (wi = next.fetch_add(1)) < rows.size() * chunks;) {
+      const uint32_t y = rows[wi / chunks];
+      const uint32_t c0 = static_cast<uint32_t>(wi % chunks) * chunk;
+      for (uint32_t c = c0; c < c0 + chunk && c < cols; ++c) {
+        const uint32_t x = c * col_step;
         const uint32_t pixel = y * width + x;
         Vec3 col = Vec3::zero();
         Rng rng(seed, pixel, 0);
@@ -780,7 +787,7 @@ int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, ui
       counters->hits += c.hits;
       counters->scatters += c.scatters;
     }
-    counters->samples = uint64_t(rows.size()) * width * spp;
+    counters->samples = uint64_t(rows.size()) * cols * spp;
   }
   return int64_t(rows.size());
 }

@@ -50,8 +50,8 @@ def lib():
         L.oracle_closest_hit.argtypes = [C.POINTER(OrPrim), C.c_uint32, f3, f3, f3]
         L.oracle_closest_hit.restype = C.c_int
         L.oracle_render.argtypes = [C.POINTER(OrPrim), C.c_uint32, C.POINTER(OrCamera), C.c_uint32, C.c_uint32,
-                                    C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
-                                    f3, C.POINTER(C.c_uint8), C.POINTER(OrCounters)]
+                                    C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                    C.c_uint32, C.c_int, f3, C.POINTER(C.c_uint8), C.POINTER(OrCounters)]
         L.oracle_render.restype = C.c_int64
         _lib = L
     return _lib
@@ -130,14 +130,15 @@ def closest_hit(prims, o, d):
 
 
 def render(prims, cam, width, height, spp, max_depth, seed=0x5EED, shard_index=0, shard_count=1, row_step=1,
-           threads=1):
-    """save_image semantics over a row subset; returns (mean[H,W,3] f32 (NaN where not
-    rendered), u8[H,W,3], counters dict, rows rendered)"""
+           threads=1, col_step=1):
+    """save_image semantics over a row subset (every col_step-th pixel of those rows);
+    returns (mean[H,W,3] f32 (NaN where not rendered), u8[H,W,3], counters dict, rows
+    rendered)"""
     mean = np.full((height, width, 3), np.nan, dtype=np.float32)
     u8 = np.zeros((height, width, 3), dtype=np.uint8)
     cnt = OrCounters()
     rows = lib().oracle_render(prims_to_c(prims), len(prims), C.byref(cam), width, height, spp, max_depth, seed,
-                               shard_index, shard_count, row_step, threads,
+                               shard_index, shard_count, row_step, col_step, threads,
                                mean.ctypes.data_as(C.POINTER(C.c_float)),
                                u8.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(cnt))
     if rows < 0:

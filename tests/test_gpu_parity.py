@@ -30,6 +30,8 @@ def assert_parity(mean, u8, st, omean, ou8, ocnt, rows=None):
     assert np.array_equal(u8, ou8), f"u8 differs at {np.argwhere(u8 != ou8)[:5]}"
     if ocnt is not None:
         assert (st["segments"], st["hits"]) == (ocnt["segments"], ocnt["hits"])
+        if "scatters" in ocnt:
+            assert st["scatters"] == ocnt["scatters"]
     return err
 
 
@@ -330,15 +332,59 @@ def test_update_and_save_image_mirror(gpu, tmp_path):
     assert out.read_bytes()[:8] == b"\x89PNG\r\n\x1a\n" and st["samples"] == w * h * 3
 
 
+def test_update_frames_reuse_one_context(gpu):
+    """tracer.rs:30-55 as a frame loop: every update() runs on the model's one fr_ctx (same
+    handle and the same device output buffers across frames, so no per-frame context or
+    buffer allocation), and each 1-spp frame equals the oracle's render of the orbited
+    camera with that frame's RNG key."""
+    import ctypes as C
+    w, h = 40, 30
+    m = gpu.create_model(w, h)
+    ocam = O.camera_new(w, h)
+    handles, buffers = set(), set()
+    for frame, keys in enumerate([0b001000, 0b000100, 0b100000, 0b000001, 0b010010]):
+        pix = gpu.update(m, keys, 0.1)
+        handles.add(m.ctx._h.value)
+        buffers.add(m.ctx.device_buffers())
+        d = (C.c_float * 3)()
+        gpu.check(gpu.lib().fr_update_delta(keys, 0.1, d))
+        O.camera_orbit(ocam, list(d))
+        assert np.array_equal(m.scene.camera.to_array(), O.camera_to_array(ocam))
+        seed = m.seed ^ (0x9E3779B97F4A7C15 * (frame + 1) & 0xFFFFFFFFFFFFFFFF)
+        _, ou8, ocnt, _ = O.render(S.BUILTIN[0](), ocam, w, h, 1, 50, seed=seed)
+        assert np.array_equal(pix.reshape(h, w, 3), ou8), frame
+        assert (m.last_stats["segments"], m.last_stats["hits"]) == (ocnt["segments"], ocnt["hits"])
+    assert len(handles) == 1 and len(buffers) == 1
+    m.close()
+
+
 # ---- full-size configurations (BASELINE.json configs), row subsets --------------
 
 def _rows(h, step):
     return list(range(0, h, step))
 
 
+def test_c1_full_frame(gpu):
+    """BASELINE config C1 (scene_01 at 256x256, 4 spp, 4 bounces), the reference's
+    CPU-runnable case, rendered whole on the GPU and by the oracle: all 65,536 pixels
+    (262,144 samples) compared, with the segment, hit and scatter counters."""
+    name, w, h, spp, depth = "scene_01", 256, 256, 4, 4
+    sc = gpu.Scene.from_file(gpu.scene_path(name), w, h)
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
+    assert st["samples"] == w * h * spp == 262144
+    prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path(name)).read())
+    cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
+    omean, ou8, ocnt, n = O.render(prims, cam, w, h, spp, depth, threads=16)
+    assert n == h
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
+
+
 @pytest.mark.slow
-@pytest.mark.parametrize("cfg", [("scene_08", 1920, 1080, 256, 8, 97), ("scene_01", 1920, 1080, 64, 8, 61)])
+@pytest.mark.parametrize("cfg", [("scene_08", 1920, 1080, 256, 8, 33), ("scene_01", 1920, 1080, 64, 8, 33)])
 def test_full_size_configs_on_row_subsets(gpu, cfg):
+    """C3 (headline) and C2 at full size: every 33rd row (33 of 1,080 rows, all 1,920
+    pixels each; 63,360 pixels) compared with the oracle."""
     name, w, h, spp, depth, step = cfg
     sc = gpu.Scene.from_file(gpu.scene_path(name), w, h)
     mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
@@ -348,11 +394,12 @@ def test_full_size_configs_on_row_subsets(gpu, cfg):
     # the oracle renders every `step`-th row of the full image (row_step over shard 0 of 1)
     omean, ou8, ocnt, n = O.render(prims, cam, w, h, spp, depth, row_step=step, threads=16)
     rows = _rows(h, step)
-    assert n == len(rows)
+    assert n == len(rows) == 33
     assert_parity(mean, u8, st, omean, ou8, None, rows=rows)
     # size-independent properties of the whole frame
     assert np.isfinite(mean).all() and (mean >= 0).all() and (mean <= 1).all()
     assert st["hits"] <= st["segments"] <= st["samples"] * (depth + 1)
+    assert st["scatters"] <= st["hits"]
 
 
 # ---- BVH (scenes of >= 48 primitives, <= 32 planes) -------------
@@ -412,9 +459,12 @@ def bvh_scene(seed, n=400, dup=True, planes=0):
     return prims
 
 
-@pytest.mark.parametrize("seed,planes", [(0, 0), (1, 0), (2, 0), (3, 0), (4, 1), (5, 3), (6, 12)])
-def test_bvh_matches_list_order_loop(gpu, seed, planes, monkeypatch):
-    w, h, spp, depth = 48, 32, 3, 8
+@pytest.mark.parametrize("seed,planes,depth", [(0, 0, 8), (1, 0, 8), (2, 0, 8), (3, 0, 8), (4, 1, 8), (5, 3, 8),
+                                               (6, 12, 8), (0, 0, 12), (5, 3, 12), (1, 0, 50), (6, 12, 50)])
+def test_bvh_matches_list_order_loop(gpu, seed, planes, depth, monkeypatch):
+    """Depth 8 runs the u16-stack BVH kernels (MAXD = 8); 12 and 50 the u32-stack ones
+    (MAXD = 0, which place the traversal stack after max_depth levels)."""
+    w, h, spp = 48, 32, 3
     prims = bvh_scene(seed, planes=planes)
     assert bvh_cost(prims) >= 48 and len(prims) >= 48  # so the product takes the BVH path
     sc = gpu.Scene.from_prims(prims)
@@ -430,15 +480,43 @@ def test_bvh_matches_list_order_loop(gpu, seed, planes, monkeypatch):
     assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
 
 
-def test_bvh_generator_10k_spheres_small(gpu):
+def test_bvh_far_origins_from_stale_plane_records(gpu, monkeypatch):
+    """Planes listed after the other primitives, small and in every orientation: a plane
+    whose denominator gate passes (plane.rs:26) but whose bounds test fails still writes
+    t (plane.rs:27-40), so the scatter origin p = o + t_stale d of the earlier winner can
+    lie thousands of scene extents away, where the BVH's node cull is not conservative.
+    Waves with such an origin walk the list in order (render.hip); the image must equal
+    the list-order loop (FR_BVH=0) and the oracle bit for bit."""
+    prims = bvh_scene(7, n=300)[:-1]  # no ground sphere: the scene extent stays small
+    r = np.random.default_rng(7)
+    for _ in range(16):
+        o = r.standard_normal(3)
+        c = r.uniform(-6, 6, 3) + np.array([0, 0, -8.0])
+        prims.append(S.plane(c, o, r.uniform(0.2, 1.0, 3), int(r.integers(0, 2)), r.uniform(0.1, 1.0, 3), 0.3))
+    assert bvh_cost(prims) >= 48
+    w, h, spp, depth = 48, 32, 6, 8
+    cam = gpu.camera_new(w, h)
+    gpu.camera_orbit(cam, (0.4, 0.1, 1.5))
+    ocam = O.camera_new(w, h)
+    O.camera_orbit(ocam, (0.4, 0.1, 1.5))
+    mean, u8, st = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=31)
+    omean, ou8, ocnt, _ = O.render(prims, ocam, w, h, spp, depth, seed=31, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    monkeypatch.setenv("FR_BVH", "0")
+    mean0, _, st0 = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=31)
+    assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
+
+
+@pytest.mark.parametrize("depth", [8, 12, 50])
+def test_bvh_generator_10k_spheres_small(gpu, depth):
     """C5's scene (tools/gen_scene.py --count 10000 --mesh sphere) at a size the oracle's
-    brute-force loop finishes quickly."""
+    brute-force loop finishes quickly; depth 12 and 50 run the u32-stack kernels."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("gen_scene", os.path.join(ROOT, "tools", "gen_scene.py"))
     gs = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(gs)
     text = gs.dumps(gs.generator_scene(10000, "sphere"))
-    w, h, spp, depth = 48, 27, 2, 8
+    w, h, spp = 48, 27, 2
     sc = gpu.Scene.from_json(text, w, h)
     assert len(sc) == 10000
     mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
@@ -558,8 +636,9 @@ def test_c4_shard_on_row_subset(gpu):
 
 @pytest.mark.slow
 def test_c5_generator_scene_on_row_subset(gpu):
-    """C5 (10k spheres, 1920x1080, 512 spp, 8 bounces, BVH path) on two rows the oracle's
-    brute-force list loop renders."""
+    """C5 (10k spheres, 1920x1080, 512 spp, 8 bounces, BVH path) against the oracle's
+    brute-force list loop on 8 rows spread over the image (every 135th row) and every 4th
+    pixel of them: 3,840 pixels, 1.97 M samples."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("gen_scene", os.path.join(ROOT, "tools", "gen_scene.py"))
     gs = importlib.util.module_from_spec(spec)
@@ -570,10 +649,12 @@ def test_c5_generator_scene_on_row_subset(gpu):
     mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
     prims, (frm, at, vup, fov) = S.load_json(text)
     cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
-    omean, ou8, _, n = O.render(prims, cam, w, h, spp, depth, row_step=539, threads=16)
-    rows = list(range(0, h, 539))
-    assert n == len(rows)
-    assert_parity(mean, u8, st, omean, ou8, None, rows=rows)
+    omean, ou8, _, n = O.render(prims, cam, w, h, spp, depth, row_step=135, col_step=4, threads=16)
+    rows = list(range(0, h, 135))
+    assert n == len(rows) == 8
+    cols = list(range(0, w, 4))
+    sub = np.ix_(rows, cols)
+    assert_parity(mean[sub], u8[sub], st, omean[sub], ou8[sub], None)
     assert np.isfinite(mean).all()
 
 
