@@ -215,7 +215,10 @@ constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for smal
 // buffer: 4 x 12 B = three 16-B stores per 4 samples instead of four scattered 12-B
 // stores, which L2 wrote back as partial lines (3.5x WRITE_SIZE). The BVH kernels keep
 // their LDS for the traversal stack (occupancy) and store each sample directly.
-__host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? 1u : 4u; }
+#ifndef FR_STAGE
+#define FR_STAGE 4  // 1 or 4 (A/B builds)
+#endif
+__host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? 1u : FR_STAGE; }
 
 // FR_DIAG builds count, per phase, wave-level trips (one per SIMT pass of the wave)
 // and lane-level work, to measure SIMT efficiency. Never enabled in the product.
@@ -872,16 +875,59 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 
 // Adds each pixel's sample colours of this pass, in sample order, onto its running
 // sum (tracer.rs:174); the last pass divides by spp, gamma-corrects and quantises
-// (tracer.rs:177-184). One thread per pixel slot; reads are coalesced across slots.
-__global__ __launch_bounds__(256) void sum_kernel(KParams kp, const float* __restrict__ samples,
-                                                  float* __restrict__ running, float* __restrict__ out_mean,
-                                                  uint8_t* __restrict__ out_u8, int first, int last) {
-  const uint32_t q = blockIdx.x * 256u + threadIdx.x;
-  if (q >= kp.P) return;
-  uint32_t x, y;
-  if (!slot_xy(kp, q, x, y)) return;
+// (tracer.rs:177-184). One thread per pixel slot. A workgroup's 256 slots of one sample
+// block are one contiguous run of the item-major buffer (256 x 192 B at ks = 16): it is
+// read with coalesced 16-B loads into LDS, padded to an odd slot stride so that each
+// thread's reads of its own slot are bank-conflict free, then summed in sample order.
+constexpr uint32_t kSumThreads = 256;
+constexpr uint32_t kSumSlot = 3 * kBlockSamples + 1;  // floats per slot in LDS (odd stride)
+
+__global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const float* __restrict__ samples,
+                                                          float* __restrict__ running, float* __restrict__ out_mean,
+                                                          uint8_t* __restrict__ out_u8, int first, int last) {
+  __shared__ float tile[kSumThreads * kSumSlot];
+  const uint32_t t = threadIdx.x;
+  const uint32_t q0 = blockIdx.x * kSumThreads, q = q0 + t;
+  const uint32_t nq = min(kSumThreads, kp.P - q0);
+  uint32_t x = 0, y = 0;
+  const bool valid = q < kp.P && slot_xy(kp, q, x, y);
   const bool mt = (kp.flags & FR_FLAG_MT_BANDS) != 0;
-  if (mt && !(kp.band_h && y / kp.band_h < 4u)) {  // rows render_mt never fills stay 0
+  const bool mt_zero = mt && !(kp.band_h && y / kp.band_h < 4u);  // rows render_mt never fills stay 0
+  V3 sum = (first || !valid) ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
+  const float fspp = static_cast<float>(kp.spp);
+  const uint32_t per = 3u * kp.ks;  // floats per slot in the buffer
+  for (uint32_t bl = 0; bl < kp.nb; ++bl) {
+    const float* src = samples + 3 * (static_cast<size_t>(bl * kp.P + q0) * kp.ks);
+    __syncthreads();  // the previous block's reads are done
+    if (kp.ks == kBlockSamples) {
+      const float4* src4 = reinterpret_cast<const float4*>(src);  // 192-B slots: 16-B aligned
+      for (uint32_t i = t; i < nq * (3u * kBlockSamples / 4u); i += kSumThreads) {
+        const float4 v = src4[i];
+        const uint32_t slot = i / 12u, w = (i - slot * 12u) * 4u;
+        float* d = tile + slot * kSumSlot + w;
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+      }
+    } else {
+      for (uint32_t i = t; i < nq * per; i += kSumThreads) tile[(i / per) * kSumSlot + i % per] = src[i];
+    }
+    __syncthreads();
+    if (valid && !mt_zero) {
+      const uint32_t n = min(kBlockSamples, kp.spp - (kp.b0 + bl) * kBlockSamples);
+      const float* c = tile + t * kSumSlot;
+      for (uint32_t j = 0; j < n; ++j, c += 3) {
+        if (mt)  // save_image_mt (tracer.rs:140-145): acc += (sqrt(c) * 255) as u8 / sample
+          sum = add(sum, V3{static_cast<float>(to_u8(c[0])) / fspp, static_cast<float>(to_u8(c[1])) / fspp,
+                            static_cast<float>(to_u8(c[2])) / fspp});
+        else
+          sum = add(sum, V3{c[0], c[1], c[2]});
+      }
+    }
+  }
+  if (!valid) return;
+  if (mt_zero) {
     if (last) {
       const size_t idx = (static_cast<size_t>(y) * kp.W + x) * 3u;
       for (int ch = 0; ch < 3; ++ch) {
@@ -890,21 +936,6 @@ __global__ __launch_bounds__(256) void sum_kernel(KParams kp, const float* __res
       }
     }
     return;
-  }
-  V3 sum = first ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
-  const float fspp = static_cast<float>(kp.spp);
-  for (uint32_t bl = 0; bl < kp.nb; ++bl) {
-    // the item's samples are contiguous (item-major buffer, KWork::samples)
-    const uint32_t s0 = (kp.b0 + bl) * kBlockSamples;
-    const uint32_t n = min(kBlockSamples, kp.spp - s0);
-    const float* c = samples + 3 * (static_cast<size_t>(bl * kp.P + q) * kp.ks);
-    for (uint32_t j = 0; j < n; ++j, c += 3) {
-      if (mt)  // save_image_mt (tracer.rs:140-145): acc += (sqrt(c) * 255) as u8 / sample
-        sum = add(sum, V3{static_cast<float>(to_u8(c[0])) / fspp, static_cast<float>(to_u8(c[1])) / fspp,
-                          static_cast<float>(to_u8(c[2])) / fspp});
-      else
-        sum = add(sum, V3{c[0], c[1], c[2]});
-    }
   }
   if (!last) {
     running[3 * q] = sum.x;
@@ -1474,7 +1505,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   HIPCHK(hipEventRecord(c->ev_start, c->stream));
   HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
   HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_start, 0));
-  const uint32_t sum_blocks = (kp.P + 255u) / 256u;
+  const uint32_t sum_blocks = (kp.P + kSumThreads - 1u) / kSumThreads;
   int traced = 0;  // trace launches whose events were recorded
   int summed = 0;
   for (int pass = 0; pass < passes || (pass == 0 && kp.P); ++pass) {
@@ -1502,7 +1533,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
     }
     const int first = pass == 0, last = pass + 1 >= passes;
     if (first && c->copy_pending) HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_copy, 0));  // last gather done
-    hipLaunchKernelGGL(sum_kernel, dim3(sum_blocks ? sum_blocks : 1u), dim3(256), 0, c->stream_sum, kp, samples,
+    hipLaunchKernelGGL(sum_kernel, dim3(sum_blocks ? sum_blocks : 1u), dim3(kSumThreads), 0, c->stream_sum, kp, samples,
                        c->d_running, c->d_mean, c->d_u8, first, last);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev_sum[pass], c->stream_sum));

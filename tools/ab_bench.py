@@ -22,11 +22,12 @@ sc = fr.Scene.from_file(fr.scene_path(scene), w, h)
 ctx = fr.RenderContext(0)
 p = fr.make_params(w, h, spp, depth, shard_index=0, shard_count=shards)
 ctx.render(sc, sc.camera, p); ctx.sync()
-ms = []
+ms, tr = [], []
 for _ in range(steps):
-    ctx.render(sc, sc.camera, p); ms.append(ctx.sync()["kernel_ms"])
+    ctx.render(sc, sc.camera, p); st = ctx.sync(); ms.append(st["kernel_ms"]); tr.append(st["trace_ms"])
 mean, u8 = ctx.download(w, h)
-print(json.dumps({"ms": sorted(ms)[len(ms)//2], "sha": hashlib.sha256(mean.tobytes()).hexdigest()[:16]}))
+print(json.dumps({"ms": sorted(ms)[len(ms)//2], "trace_ms": sorted(tr)[len(tr)//2],
+                  "sha": hashlib.sha256(mean.tobytes()).hexdigest()[:16]}))
 '''
 
 
@@ -43,6 +44,7 @@ def main():
     a = ap.parse_args()
     w, h = map(int, a.size.split("x"))
     res = {lib: [] for lib in a.libs}
+    trace = {lib: [] for lib in a.libs}
     shas = {}
     for _ in range(a.reps):
         for lib in a.libs:
@@ -59,12 +61,14 @@ def main():
                 sys.exit(1)
             r = json.loads(out.stdout.strip().splitlines()[-1])
             res[lib].append(r["ms"])
+            trace[lib].append(r.get("trace_ms", 0.0))
             shas[lib] = r["sha"]
     base = shas[a.libs[0]]
     for lib in a.libs:
         ms = sorted(res[lib])[len(res[lib]) // 2]
+        tms = sorted(trace[lib])[len(trace[lib]) // 2]
         samples = w * h * a.spp / a.shards
-        print(f"{os.path.basename(lib):40s} {ms:9.3f} ms  {samples / ms / 1e3:10.1f} Msamples/s  "
+        print(f"{os.path.basename(lib):40s} {ms:9.3f} ms (trace {tms:8.3f})  {samples / ms / 1e3:10.1f} Msamples/s  "
               f"{'same image' if shas[lib] == base else 'IMAGE DIFFERS ' + shas[lib]}")
 
 
