@@ -346,7 +346,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   uint4* hrow = reinterpret_cast<uint4*>(stack) + tid;  // this lane's MAXD = 8 levels
   // BVH traversal stack, after the unwind stack: kBvhStack x kBlock u32 (level-major)
   uint32_t* tstack = stack + (MAXD ? (MAXD * kBlock) / 2u : (kp.max_depth ? kp.max_depth : 1u) * kBlock);
-  const uint32_t unit2 = sc.n | (sc.n << 16);            // two empty levels
+  // MAXD > 0 stack entries: with the attenuations in LDS, the entry's byte offset in
+  // att_lds (n_att <= kAttLds, so < 2^16), read by the unwind without index arithmetic;
+  // otherwise the primitive index
+  const uint32_t ent_shift = n_att ? 4u : 0u;
+  const uint32_t unit_ent = sc.n << ent_shift;
+  const uint32_t unit2 = unit_ent | (unit_ent << 16);  // two empty levels
   if (MAXD > 0) *hrow = make_uint4(unit2, unit2, unit2, unit2);
   for (uint32_t i = tid; i < n_att_st; i += kBlock) {
     const float4 a = sc.att[i];
@@ -372,7 +377,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // stack push at level `depth` of the scatter winner
   auto push = [&](uint32_t pi) {
     if (MAXD > 0)
-      hstack[tid * MAXD + depth] = static_cast<uint16_t>(pi);
+      hstack[tid * MAXD + depth] = static_cast<uint16_t>(pi << ent_shift);
     else
       stack[depth * kBlock + tid] = pi;
   };
@@ -383,7 +388,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   V3 sn{0.0f, 0.0f, 0.0f};  // metal: normal
   float sfuzz = 0.0f, fx = 0.0f, fy = 0.0f, vofs = 0.0f;
   bool smetal = false;
-  uint32_t sbest = 0, q = 0, s = 0, s_end = 0, nseg = 0, nhit = 0, nscat = 0;
+  uint32_t sbest = 0, s = 0, s_end = 0, nseg = 0, nhit = 0, nscat = 0;
   uint32_t jj = 0;           // sample index within the item's block
   float* out = kw.samples;   // the item's first sample slot (item-major buffer)
   Rng rng{0u, 0u, 0u, 0u};
@@ -402,6 +407,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // multiplies) runs once per 64 items at full width instead of in every iteration in
   // which a lane or two claim; a claiming lane fetches its stream by a lane permute.
   Rng held{0u, 0u, 0u, 0u};
+  // ... and the same slot's pixel (x | y << 16, all ones past the image edge) and sample
+  // block, so a claiming lane fetches those by permute too instead of dividing the item
+  uint32_t held_xy = 0xFFFFFFFFu, held_b = 0u;
   while (active) {
     DIAG_WAVE(DG_ITER);
     const unsigned long long m = __ballot(need_item);
@@ -419,6 +427,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       const bool grab = n > avail;
       const int first = __ffsll(static_cast<long long>(m)) - 1;
       Rng src = held;  // slots [64 - avail, 64) still hold the current batch's streams
+      uint32_t src_xy = held_xy, src_b = held_b;
       if (grab) {
         if (static_cast<int>(lane) == first) base = atomicAdd(kw.queue, kBatch);
         base = __builtin_amdgcn_readlane(base, first);
@@ -427,9 +436,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         // drained, and from then on no batch holds a valid item. A slot past the image
         // or the queue gets a stream that is never used.
         uint32_t bb, qq, xx, yy;
-        item_xy(kp, base + lane, bb, qq, xx, yy);
+        const bool in_image = item_xy(kp, base + lane, bb, qq, xx, yy);
         held = rng_seed(kp.seed, yy * kp.W + xx, bb);
-        if (lane < kBatch - avail) src = held;  // the new batch's first slots are taken now
+        held_xy = in_image ? (xx | (yy << 16)) : 0xFFFFFFFFu;
+        held_b = bb;
+        if (lane < kBatch - avail) {  // the new batch's first slots are taken now
+          src = held;
+          src_xy = held_xy;
+          src_b = held_b;
+        }
         // Queue tail: the waves that claim last hold the longest remaining work, so they
         // get issue priority over waves finishing older items (shortens the drain).
         if (base >= kp.prio_at[0]) {
@@ -446,6 +461,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                    static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s1))),
                    static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s2))),
                    static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s3)))};
+      // (every lane of the wave is active here: a permute reads 0 from an inactive source)
+      const uint32_t xy = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src_xy)));
+      const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src_b)));
       if (need_item && item >= kp.n_items) {
 #ifdef FR_DIAG
         if (gw < 65536) atomicMin(&g_fr_wave_drain[gw], static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
@@ -454,8 +472,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         continue;
       }
       if (need_item) {
-        uint32_t b, x, y;
-        bool ok = item_xy(kp, item, b, q, x, y);
+        const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
+        bool ok = xy != 0xFFFFFFFFu;
         uint32_t yrow = kp.H - y;  // tracer.rs:171-172: v = ((H - y) + r) / H
         if (MT) {
           // render_mt (tracer.rs:86-103): band k from the top is thread t_id = 3 - k;
@@ -502,13 +520,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         DIAG_WAVE(DG_LENS_W);
         DIAG_LANE(DG_LENS_L);
         if (!acc) {
-          px = rng_signed_unit(rng);
-          py = rng_signed_unit(rng);
-          pz = sph ? rng_signed_unit(rng) : 0.0f;
-          acc = !(px * px + py * py + pz * pz >= 1.0f);
+          // the test in the 2^23-scaled domain (rng_signed_unit_scaled): same decisions
+          px = rng_signed_unit_scaled(rng);
+          py = rng_signed_unit_scaled(rng);
+          pz = sph ? rng_signed_unit_scaled(rng) : 0.0f;
+          acc = !(px * px + py * py + pz * pz >= kUnitBallScaled);
         }
       } while (lanes_set(!acc) > static_cast<uint32_t>(KREJ));
       if (acc) {
+        px *= kSignedUnitScale;  // the accepted point, 2r - 1 per coordinate (exact)
+        py *= kSignedUnitScale;
+        pz *= kSignedUnitScale;
         if (!sph) {
           // Camera::get_ray (camera.rs:62-72)
 #if !defined(FR_CAM_RESIDENT) && defined(__HIP_DEVICE_COMPILE__)
@@ -792,11 +814,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         *hrow = make_uint4(unit2, unit2, unit2, unit2);  // the next sample starts empty
         const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
         if (n_att) {
+          const char* att_bytes = reinterpret_cast<const char*>(att_lds);
 #pragma unroll
           for (int j = MAXD - 1; j >= 0; --j) {
             DIAG_WAVE(DG_UNW_W);
-            const uint32_t pi = (ws[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-            col = mul(xyz(att_lds[pi]), col);
+            const uint32_t off = (j & 1) ? (ws[j >> 1] >> 16) : (ws[j >> 1] & 0xFFFFu);  // byte offset
+            col = mul(xyz(*reinterpret_cast<const float4*>(att_bytes + off)), col);
           }
         } else {
           // global attenuations: only the levels in use
@@ -1223,7 +1246,11 @@ static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t 
       per_cu < 1)
     per_cu = 1;
   *g.per_cu = per_cu;
-  const uint64_t cap = static_cast<uint64_t>(per_cu) * static_cast<uint64_t>(g.num_cus);
+  uint64_t cap = static_cast<uint64_t>(per_cu) * static_cast<uint64_t>(g.num_cus);
+  // FR_MAX_WGS=k caps the grid (tests: with a few workgroups every wave claims many
+  // batches, partly used ones included, so the claim paths run at small image sizes)
+  if (const char* e = getenv("FR_MAX_WGS"))
+    if (atoi(e) > 0 && static_cast<uint64_t>(atoi(e)) < cap) cap = static_cast<uint64_t>(atoi(e));
   const uint32_t blocks = static_cast<uint32_t>(g.want < cap ? (g.want ? g.want : 1u) : cap);
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, st, a);
 }
@@ -1281,6 +1308,8 @@ static int check_params(const fr_params* p) {
   if (p->width == 0 || p->height == 0) return set_error(FR_EARG, "width/height must be > 0");
   if (static_cast<uint64_t>(p->width) * p->height > (1ull << 31))
     return set_error(FR_EARG, "image too large (pixel index must fit in 31 bits)");
+  if (p->width > 65535 || p->height > 65535)
+    return set_error(FR_EARG, "width/height must be < 65536 (packed pixel coordinates)");
   if (p->max_depth > kMaxDepth) return set_error(FR_EARG, "max_depth %u > %u", p->max_depth, kMaxDepth);
   if (p->strip_rows != kStripRows) return set_error(FR_EARG, "strip_rows must be %u", kStripRows);
   if (p->shard_count == 0 || p->shard_index >= p->shard_count)

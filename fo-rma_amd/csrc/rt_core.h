@@ -117,6 +117,15 @@ FR_HD float rng_signed_unit(Rng& r) {
   return static_cast<float>(static_cast<int32_t>(rng_next(r)) >> 8) * 1.1920928955078125e-07f;
 }
 
+// The same value scaled by 2^23: the integer (int32)u >> 8 as an f32 (exact). A
+// rejection test on these, dot(k, k) >= 2^46, takes the same decision as dot(p, p) >= 1
+// on p = k * 2^-23: every product and sum is the unscaled one times 2^46 exactly (f32
+// rounding commutes with power-of-two scaling away from the denormal and overflow
+// ranges, and 1 <= k*k <= 2^46 or k = 0). The accepted point is scaled once.
+FR_HD float rng_signed_unit_scaled(Rng& r) { return static_cast<float>(static_cast<int32_t>(rng_next(r)) >> 8); }
+constexpr float kSignedUnitScale = 1.1920928955078125e-07f;  // 2^-23
+constexpr float kUnitBallScaled = 70368744177664.0f;         // 2^46
+
 // utility.rs:4-13: p = 2*(r1, r2, 0) - (1, 1, 0), retry while dot(p,p) >= 1
 #ifndef FR_LENS_TRY
 #define FR_LENS_TRY()

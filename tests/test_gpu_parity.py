@@ -299,6 +299,23 @@ def test_edge_cases(gpu, case):
     assert_parity(mean, u8, st, omean, ou8, ocnt)
 
 
+@pytest.mark.parametrize("wgs,scene,w,h,spp,depth", [(1, "scene_08", 64, 40, 40, 8), (3, "scene_01", 48, 32, 20, 8),
+                                                    (1, "scene_02", 40, 24, 3, 12), (2, "scene_08", 72, 16, 1, 4)])
+def test_small_grid_claims_many_batches(gpu, wgs, scene, w, h, spp, depth, monkeypatch):
+    """FR_MAX_WGS caps the persistent grid, so each wave claims many 64-item batches, one
+    or a few lanes at a time, across sample blocks and across partly used batches: the
+    claim step's lane permutes (stream, pixel, block from the seeding lane) and the queue
+    tail run at a size the oracle renders whole."""
+    monkeypatch.setenv("FR_MAX_WGS", str(wgs))
+    sc = gpu.Scene.from_file(gpu.scene_path(scene), w, h)
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
+    prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path(scene)).read())
+    cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
+    omean, ou8, ocnt, _ = O.render(prims, cam, w, h, spp, depth, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    assert st["occupancy"] >= 1
+
+
 def test_context_reuse_and_scene_edits(gpu):
     w, h = 32, 32
     sc = gpu.Scene.builtin(0, w, h)

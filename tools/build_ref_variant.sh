@@ -1,0 +1,22 @@
+#!/bin/bash
+# Build libforma_rt from the kernel sources of a git revision, for A/B timing against the
+# working tree (tools/ab_bench.py):
+#   tools/build_ref_variant.sh REV NAME [DEFS]  ->  fo-rma_amd/build/variants/libforma_rt_NAME.so
+# The host objects (scene, JSON, BVH, post) come from the working tree's build; the ABI of
+# REV must match the working tree's include/forma_rt.h.
+set -e
+rev=$1; name=$2; defs=${3:-}
+root="$(cd "$(dirname "$0")/.." && pwd)"
+tmp=$(mktemp -d)
+trap 'rm -rf "$tmp"' EXIT
+mkdir -p "$tmp/fo-rma_amd/csrc" "$tmp/include"
+git -C "$root" archive "$rev" fo-rma_amd/csrc include | tar -x -C "$tmp"
+make -C "$root/fo-rma_amd" -s build/scene.o build/json_min.o build/bvh.o build/post.o
+mkdir -p "$root/fo-rma_amd/build/variants"
+FP="-ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP -fno-slp-vectorize $defs \
+  -c "$tmp/fo-rma_amd/csrc/render.hip" -o "$tmp/render.o"
+b="$root/fo-rma_amd/build"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$b/variants/libforma_rt_$name.so" "$tmp/render.o" \
+  "$b/scene.o" "$b/json_min.o" "$b/bvh.o" "$b/post.o"
+echo "$b/variants/libforma_rt_$name.so"
