@@ -64,6 +64,17 @@ constexpr uint32_t kMaxDepth = 64;    // LDS stack bound (64 KB per workgroup)
 #define FR_NUM_SGPR 96
 #endif
 constexpr uint32_t kSmallDepth = 8;
+// Deferred unwind (DEFER kernels: depth <= 8, <= kDeferMaxPrims primitives, no BVH, not
+// render_mt): a path's sample slot holds the record {t, winners 0-3, winners 4-7} instead
+// of its colour: t = the sky blend parameter 0.5 (unit(d).y + 1) of the escaping ray, or
+// kDeferAbsorbed (-1, which no t in [0, 1] or NaN equals) for a path that returns 0; the
+// winners as u8 primitive indices, kDeferUnit on empty levels. sum_kernel rebuilds
+// a0 * (a1 * (... * term)) from it in the same order, at full SIMD width instead of in the
+// few lanes whose paths end in a given iteration.
+constexpr uint32_t kDeferMaxPrims = 254;
+constexpr uint32_t kDeferUnit = 255;
+constexpr uint32_t kDeferAbsorbed = 0xBF800000u;  // -1.0f
+constexpr uint32_t KF_DEFER = 1u << 31;            // internal KParams.flags bit: records, not colours
 #ifndef FR_BLOCK_SAMPLES
 #define FR_BLOCK_SAMPLES 16  // RNG contract: one stream per 16-sample block (oracle.cpp agrees)
 #endif
@@ -312,7 +323,7 @@ enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 // amdgpu_num_sgpr caps the scalar registers (MI355X_MICROARCH.md "Residency and
 // cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
 // admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
-template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT>
+template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, bool DEFER>
 #ifdef FR_WAVES_PER_EU
 #define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU, FR_WAVES_PER_EU)))
 #else
@@ -343,6 +354,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   static_assert(MAXD == 0 || MAXD == 8, "the u16 stack is one 16-B row per lane");
+  static_assert(!DEFER || (MAXD == 8 && !BVH && !MT), "deferred unwind: depth <= 8 list kernels");
+  uint2* drow = reinterpret_cast<uint2*>(stack) + tid;  // DEFER: this lane's 8 u8 levels
+  uint8_t* bstack = reinterpret_cast<uint8_t*>(stack);
   uint4* hrow = reinterpret_cast<uint4*>(stack) + tid;  // this lane's MAXD = 8 levels
   // BVH traversal stack, after the unwind stack: kBvhStack x kBlock u32 (level-major)
   uint32_t* tstack = stack + (MAXD ? (MAXD * kBlock) / 2u : (kp.max_depth ? kp.max_depth : 1u) * kBlock);
@@ -352,7 +366,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   const uint32_t ent_shift = n_att ? 4u : 0u;
   const uint32_t unit_ent = sc.n << ent_shift;
   const uint32_t unit2 = unit_ent | (unit_ent << 16);  // two empty levels
-  if (MAXD > 0) *hrow = make_uint4(unit2, unit2, unit2, unit2);
+  if (DEFER)
+    *drow = make_uint2(~0u, ~0u);
+  else if (MAXD > 0)
+    *hrow = make_uint4(unit2, unit2, unit2, unit2);
   for (uint32_t i = tid; i < n_att_st; i += kBlock) {
     const float4 a = sc.att[i];
     att_lds[i] = make_float4(a.x, a.y, a.z, __uint_as_float(i < n_att ? sc.cls[i] : 0u));
@@ -376,7 +393,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   uint32_t depth = 0;
   // stack push at level `depth` of the scatter winner
   auto push = [&](uint32_t pi) {
-    if (MAXD > 0)
+    if (DEFER)
+      bstack[tid * 8u + depth] = static_cast<uint8_t>(pi);
+    else if (MAXD > 0)
       hstack[tid * MAXD + depth] = static_cast<uint16_t>(pi << ent_shift);
     else
       stack[depth * kBlock + tid] = pi;
@@ -511,6 +530,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     PROF_MARK(PF_CLAIM);
     bool ended = false;
     V3 term{0.0f, 0.0f, 0.0f};
+    uint32_t tsky = kDeferAbsorbed;  // DEFER: the terminal as sky parameter bits
     if (need != NEED_NONE) {
       // 1. merged rejection loop
       float px = 0.0f, py = 0.0f, pz = 0.0f;
@@ -726,7 +746,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       }
       PROF_MARK(PF_HIT);
       if (best < 0) {
-        term = sky(d);  // tracer.rs:211-218
+        if (DEFER)
+          tsky = __float_as_uint(sky_t(d));  // tracer.rs:211-218, the blend in sum_kernel
+        else
+          term = sky(d);  // tracer.rs:211-218
         ended = true;
         have_ray = false;
       } else {
@@ -806,7 +829,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       DIAG_WAVE(DG_END_W);
       DIAG_LANE(DG_END_L);
       V3 col = term;
-      if (MAXD > 0) {
+      if (DEFER) {
+        const uint2 w = *drow;
+        *drow = make_uint2(~0u, ~0u);  // the next sample starts empty
+        col = V3{__uint_as_float(tsky), __uint_as_float(w.x), __uint_as_float(w.y)};
+      } else if (MAXD > 0) {
         // One read brings the lane's 8 levels; empty ones point at the unit entry
         // (x * 1.0f == x), so the product a0*(a1*(...*term)) needs no per-level branch
         // and its reads do not wait on each other.
@@ -900,16 +927,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 // sum (tracer.rs:174); the last pass divides by spp, gamma-corrects and quantises
 // (tracer.rs:177-184). One thread per pixel slot. A workgroup's 256 slots of one sample
 // block are one contiguous run of the item-major buffer (256 x 192 B at ks = 16): it is
-// read with coalesced 16-B loads into LDS, padded to an odd slot stride so that each
-// thread's reads of its own slot are bank-conflict free, then summed in sample order.
+// read with coalesced 16-B loads into an LDS tile whose odd slot stride keeps each
+// thread's reads of its own slot bank-conflict free, then summed in sample order. With
+// KF_DEFER the slots hold deferred-unwind records (kDeferUnit) and the colour is rebuilt
+// here from a 12-B-per-entry attenuation table (tile + table fit three workgroups per CU).
 constexpr uint32_t kSumThreads = 256;
 constexpr uint32_t kSumSlot = 3 * kBlockSamples + 1;  // floats per slot in LDS (odd stride)
 
 __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const float* __restrict__ samples,
                                                           float* __restrict__ running, float* __restrict__ out_mean,
-                                                          uint8_t* __restrict__ out_u8, int first, int last) {
+                                                          uint8_t* __restrict__ out_u8, int first, int last,
+                                                          const float4* __restrict__ att, uint32_t n_prims) {
   __shared__ float tile[kSumThreads * kSumSlot];
+  __shared__ float att_s[3 * (kDeferUnit + 1)];  // KF_DEFER: attenuation rgb, entry kDeferUnit = 1
   const uint32_t t = threadIdx.x;
+  const bool defer = (kp.flags & KF_DEFER) != 0;
+  if (defer) {  // kSumThreads == kDeferUnit + 1
+    const float4 a = t < n_prims ? att[t] : make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    att_s[3 * t] = a.x;
+    att_s[3 * t + 1] = a.y;
+    att_s[3 * t + 2] = a.z;
+  }
   const uint32_t q0 = blockIdx.x * kSumThreads, q = q0 + t;
   const uint32_t nq = min(kSumThreads, kp.P - q0);
   uint32_t x = 0, y = 0;
@@ -921,17 +959,29 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   const uint32_t per = 3u * kp.ks;  // floats per slot in the buffer
   for (uint32_t bl = 0; bl < kp.nb; ++bl) {
     const float* src = samples + 3 * (static_cast<size_t>(bl * kp.P + q0) * kp.ks);
-    __syncthreads();  // the previous block's reads are done
+    __syncthreads();  // the previous block's reads are done (and the table is written)
     if (kp.ks == kBlockSamples) {
+      // all twelve 16-B loads in flight before the LDS writes
       const float4* src4 = reinterpret_cast<const float4*>(src);  // 192-B slots: 16-B aligned
-      for (uint32_t i = t; i < nq * (3u * kBlockSamples / 4u); i += kSumThreads) {
-        const float4 v = src4[i];
-        const uint32_t slot = i / 12u, w = (i - slot * 12u) * 4u;
-        float* d = tile + slot * kSumSlot + w;
-        d[0] = v.x;
-        d[1] = v.y;
-        d[2] = v.z;
-        d[3] = v.w;
+      constexpr uint32_t kV = 3u * kBlockSamples / 4u;             // float4 per slot
+      const uint32_t n4 = nq * kV;
+      float4 v[kV];
+#pragma unroll
+      for (uint32_t k = 0; k < kV; ++k) {
+        const uint32_t i = t + k * kSumThreads;
+        if (i < n4) v[k] = src4[i];
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kV; ++k) {
+        const uint32_t i = t + k * kSumThreads;
+        if (i < n4) {
+          const uint32_t slot = i / kV, w = (i - slot * kV) * 4u;
+          float* d = tile + slot * kSumSlot + w;
+          d[0] = v[k].x;
+          d[1] = v[k].y;
+          d[2] = v[k].z;
+          d[3] = v[k].w;
+        }
       }
     } else {
       for (uint32_t i = t; i < nq * per; i += kSumThreads) tile[(i / per) * kSumSlot + i % per] = src[i];
@@ -941,11 +991,22 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
       const uint32_t n = min(kBlockSamples, kp.spp - (kp.b0 + bl) * kBlockSamples);
       const float* c = tile + t * kSumSlot;
       for (uint32_t j = 0; j < n; ++j, c += 3) {
-        if (mt)  // save_image_mt (tracer.rs:140-145): acc += (sqrt(c) * 255) as u8 / sample
+        if (defer) {
+          // the deferred unwind (kDeferUnit): terminal, then a_7 ... a_0 innermost first
+          const uint32_t tb = __float_as_uint(c[0]), lo = __float_as_uint(c[1]), hi = __float_as_uint(c[2]);
+          V3 col = tb == kDeferAbsorbed ? V3{0.0f, 0.0f, 0.0f} : sky_from_t(c[0]);
+#pragma unroll
+          for (int k = 7; k >= 0; --k) {
+            const float* e = att_s + 3u * (((k >= 4 ? hi : lo) >> (8 * (k & 3))) & 0xFFu);
+            col = mul(V3{e[0], e[1], e[2]}, col);
+          }
+          sum = add(sum, col);
+        } else if (mt) {  // save_image_mt (tracer.rs:140-145): acc += (sqrt(c) * 255) as u8 / sample
           sum = add(sum, V3{static_cast<float>(to_u8(c[0])) / fspp, static_cast<float>(to_u8(c[1])) / fspp,
                             static_cast<float>(to_u8(c[2])) / fspp});
-        else
+        } else {
           sum = add(sum, V3{c[0], c[1], c[2]});
+        }
       }
     }
   }
@@ -1258,10 +1319,17 @@ static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t 
 template <int KS, bool HP, bool BV, bool MT = false>
 static void launch_depth(bool small_depth, const Grid& g, size_t lds, hipStream_t st, const KScene& ks,
                          const KCam& kc, const KParams& kp, const KWork& kw) {
+  if constexpr (!BV && !MT) {
+    if (kp.flags & KF_DEFER) {
+      launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, false, false, true>, g, lds, st,
+                        KArgs{ks, kc, kp, kw});
+      return;
+    }
+  }
   if (small_depth)
-    launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV, MT>, g, lds, st, KArgs{ks, kc, kp, kw});
+    launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV, MT, false>, g, lds, st, KArgs{ks, kc, kp, kw});
   else
-    launch_persistent(trace_kernel<KS, HP, FR_KREJ, 0, BV, MT>, g, lds, st, KArgs{ks, kc, kp, kw});
+    launch_persistent(trace_kernel<KS, HP, FR_KREJ, 0, BV, MT, false>, g, lds, st, KArgs{ks, kc, kp, kw});
 }
 
 // BVH kernels walk the list's segments (bvh.h); scenes with planes use the general
@@ -1512,7 +1580,13 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   }
   const size_t n_att = dc->n <= kAttLds ? dc->n : 0u;
   const bool small_depth = p->max_depth <= kSmallDepth && dc->n < 65536u;
-  const size_t stack_bytes = small_depth ? kSmallDepth * kBlock * sizeof(uint16_t)
+  // the deferred unwind (kDeferMaxPrims); FR_DEFER=0 keeps the unwind in the trace kernel (A/B)
+  const char* defer_env = getenv("FR_DEFER");
+  const bool defer = small_depth && dc->n <= kDeferMaxPrims && !use_bvh && !(p->flags & FR_FLAG_MT_BANDS) &&
+                     !(defer_env && strcmp(defer_env, "0") == 0);
+  if (defer) kp.flags |= KF_DEFER;
+  const size_t stack_bytes = defer ? kSmallDepth * kBlock * sizeof(uint8_t)
+                           : small_depth ? kSmallDepth * kBlock * sizeof(uint16_t)
                                          : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
                                                sizeof(uint32_t);
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
@@ -1563,7 +1637,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
     const int first = pass == 0, last = pass + 1 >= passes;
     if (first && c->copy_pending) HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_copy, 0));  // last gather done
     hipLaunchKernelGGL(sum_kernel, dim3(sum_blocks ? sum_blocks : 1u), dim3(kSumThreads), 0, c->stream_sum, kp, samples,
-                       c->d_running, c->d_mean, c->d_u8, first, last);
+                       c->d_running, c->d_mean, c->d_u8, first, last, ks.att, dc->n);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev_sum[pass], c->stream_sum));
     summed = pass + 1;

@@ -402,11 +402,13 @@ FR_HD V3 scatter_dielectric(V3 d, V3 n, Rng& r) {
 }
 
 // tracer.rs:211-218
-FR_HD V3 sky(V3 d) {
+// split in two for the deferred unwind (render.hip): the blend parameter t, and the colour
+FR_HD float sky_t(V3 d) {
   const V3 ud = unit(d);
-  const float t = 0.5f * (ud.y + 1.0f);
-  return add(scl(1.0f - t, V3{1.0f, 1.0f, 1.0f}), scl(t, V3{0.5f, 0.7f, 1.0f}));
+  return 0.5f * (ud.y + 1.0f);
 }
+FR_HD V3 sky_from_t(float t) { return add(scl(1.0f - t, V3{1.0f, 1.0f, 1.0f}), scl(t, V3{0.5f, 0.7f, 1.0f})); }
+FR_HD V3 sky(V3 d) { return sky_from_t(sky_t(d)); }
 
 // tracer.rs:182-184: Rust `as u8` saturates (NaN -> 0) and truncates toward zero.
 FR_HD uint8_t to_u8(float c) {
