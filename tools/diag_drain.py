@@ -17,3 +17,9 @@ tail = e[ok] - d
 print(f"per-wave end - first drained claim: mean {tail.mean()/1e3:.3f} p50 {np.median(tail)/1e3:.3f} "
       f"p90 {np.percentile(tail, 90)/1e3:.3f} max {tail.max()/1e3:.3f} ms")
 print(f"kernel end - first drain anywhere: {(e.max() - d.min())/1e3:.3f} ms")
+# residency over time: fraction of the kernel's waves still running at each tenth
+T = e.max()
+for f in [0.5, 0.7, 0.8, 0.85, 0.9, 0.95, 0.98]:
+    tt = f * T
+    print(f"  t={tt/1e3:.3f} ms ({f:.0%}): {np.mean((s <= tt) & (e > tt)):.1%} of waves running")
+print(f"  wave starts: first {s.min()/1e3:.4f} ms, last {s.max()/1e3:.4f} ms")
