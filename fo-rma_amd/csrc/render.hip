@@ -40,6 +40,12 @@ __device__ unsigned long long g_fr_diag_rus[2];
 // per-wave start/end (s_memrealtime, 100 MHz) for the residency-over-time profile
 __device__ unsigned long long g_fr_wave_times[2 * 65536];
 __device__ unsigned long long g_fr_wave_drain[65536];  // first drained claim of the wave
+// segments traced per (sample block, tile) batch of 64 items: index item >> 6 (< 2^20 kept)
+__device__ unsigned int g_fr_tb_cost[1u << 20];
+// per wave: iterations at its first drained claim and at its end
+__device__ unsigned int g_fr_wave_iters[2 * 65536];
+// every 64th wave: the time of each of its first 1024 loop iterations (100 MHz)
+__device__ unsigned long long g_fr_iter_times[1024 * 1024];
 #define FR_LENS_TRY() FR_DIAG_TRY(g_fr_diag_lens)
 #define FR_RUS_TRY() FR_DIAG_TRY(g_fr_diag_rus)
 #endif
@@ -57,6 +63,7 @@ namespace fr {
 constexpr uint32_t kBlock = 256;      // 4 waves, one 8x8 pixel tile each
 constexpr uint32_t kStripRows = 8;    // rows per shard strip == tile height
 constexpr uint32_t kMaxDepth = 64;    // LDS stack bound (64 KB per workgroup)
+constexpr uint32_t kMaxWgPerCu = 8;   // 2048 threads per CU / kBlock: the persistent grid's cap
 #ifndef FR_KREJ
 #define FR_KREJ 4  // rejection loop: lanes left to the next iteration (tuning only, results unchanged)
 #endif
@@ -162,7 +169,10 @@ struct KWork {
   // per-sample colours, item-major: sample s of item (b, q) at [(item * ks + s - 16 b)] x 3 f32,
   // item = (b - b0) * P + q, so one item's samples are contiguous (192 B at ks = 16)
   float* samples;
-  unsigned long long* counters;  // [0] segments, [1] hits, [2] scatters
+  unsigned long long* counters;  // [0] segments, [1] hits, [2] scatters (reduce_counters)
+  // per-wave partial counters, [wave][3], stored by every wave of the grid and summed
+  // into counters by reduce_counters after the launch
+  unsigned long long* wave_counters;
 };
 
 // camera.rs fields the ray generator reads: position, lower_left_corner,
@@ -409,6 +419,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   bool smetal = false;
   uint32_t sbest = 0, s = 0, s_end = 0, nseg = 0, nhit = 0, nscat = 0;
   uint32_t jj = 0;           // sample index within the item's block
+#ifdef FR_DIAG
+  uint32_t diag_tb = 0, diag_seg0 = 0;  // the item's batch index, segments at its claim
+  uint32_t diag_iter = 0;               // loop iterations of this wave
+#endif
   float* out = kw.samples;   // the item's first sample slot (item-major buffer)
   Rng rng{0u, 0u, 0u, 0u};
   bool active = true, need_item = true, need_jit = false, have_ray = false;
@@ -431,6 +445,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   uint32_t held_xy = 0xFFFFFFFFu, held_b = 0u;
   while (active) {
     DIAG_WAVE(DG_ITER);
+#ifdef FR_DIAG
+    if (lane == 0 && (gw & 63u) == 0 && (gw >> 6) < 1024u && diag_iter < 1024u)
+      g_fr_iter_times[(gw >> 6) * 1024u + diag_iter] = __builtin_amdgcn_s_memrealtime();
+    ++diag_iter;
+#endif
     const unsigned long long m = __ballot(need_item);
     if (m) {
       // 0. claim work items: the free lanes take consecutive items of the wave's batch;
@@ -485,7 +504,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src_b)));
       if (need_item && item >= kp.n_items) {
 #ifdef FR_DIAG
-        if (gw < 65536) atomicMin(&g_fr_wave_drain[gw], static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+        if (gw < 65536) {
+          const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+          if (now < g_fr_wave_drain[gw]) {
+            g_fr_wave_drain[gw] = now;
+            g_fr_wave_iters[2 * gw] = diag_iter;
+          }
+        }
 #endif
         active = false;  // queue drained
         continue;
@@ -507,6 +532,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           s = b * kBlockSamples;
           out = kw.samples + 3 * (static_cast<size_t>(item) * kp.ks);
           jj = 0;
+#ifdef FR_DIAG
+          diag_tb = item >> 6;
+          diag_seg0 = nseg;
+#endif
           s_end = min(s + kBlockSamples, kp.spp);
           fx = static_cast<float>(x);
           fy = static_cast<float>(yrow);
@@ -892,6 +921,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         }
       }
       ++jj;
+#ifdef FR_DIAG
+      if (s + 1u == s_end && diag_tb < (1u << 20)) atomicAdd(&g_fr_tb_cost[diag_tb], nseg - diag_seg0);
+#endif
       if (++s == s_end)
         need_item = true;
       else
@@ -900,24 +932,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     PROF_MARK(PF_END);
   }
 
-  // per-wave counter reduction, one 64-bit atomic per wave per counter
+  // Per-wave counter reduction into the wave's own slot (plain stores): the waves leave
+  // the drain within a fraction of a millisecond, and three returning atomics per wave on
+  // one cache line queued long enough there to hold the kernel's end back.
   unsigned long long a = nseg, b = nhit, sct = nscat;
   for (int m = 32; m > 0; m >>= 1) {
     a += __shfl_xor(a, m);
     b += __shfl_xor(b, m);
     sct += __shfl_xor(sct, m);
   }
-  if (lane == 0 && (a | b)) {
-    atomicAdd(&kw.counters[0], a);
-    atomicAdd(&kw.counters[1], b);
-    atomicAdd(&kw.counters[2], sct);
+  if (lane == 0) {
+    unsigned long long* wc = kw.wave_counters + 3u * (blockIdx.x * (kBlock / 64u) + (tid >> 6));
+    wc[0] = a;
+    wc[1] = b;
+    wc[2] = sct;
   }
 #ifdef FR_PROF
   if (lane == 0)
     for (int k = 0; k < PF_N; ++k) atomicAdd(&kw.counters[20 + k], static_cast<unsigned long long>(pf_acc[k]));
 #endif
 #ifdef FR_DIAG
-  if (lane == 0 && gw < 65536) g_fr_wave_times[2 * gw + 1] = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && gw < 65536) {
+    g_fr_wave_times[2 * gw + 1] = __builtin_amdgcn_s_memrealtime();
+    g_fr_wave_iters[2 * gw + 1] = diag_iter;
+  }
   __syncthreads();
   if (tid < DG_N) atomicAdd(&kw.counters[4 + tid], static_cast<unsigned long long>(dg[tid]));
 #endif
@@ -1046,6 +1084,23 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
     out_u8[idx + 1] = to_u8(mean.y);
     out_u8[idx + 2] = to_u8(mean.z);
   }
+}
+
+// Sums the trace kernel's per-wave counters (KWork::wave_counters) into counters[0..2].
+__global__ __launch_bounds__(256) void reduce_counters(const unsigned long long* __restrict__ wc, uint32_t waves,
+                                                       unsigned long long* __restrict__ counters) {
+  __shared__ unsigned long long part[3][256];
+  unsigned long long v[3] = {0, 0, 0};
+  for (uint32_t w = threadIdx.x; w < waves; w += 256)
+    for (int k = 0; k < 3; ++k) v[k] += wc[3 * w + k];
+  for (int k = 0; k < 3; ++k) part[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (uint32_t h = 128; h > 0; h >>= 1) {
+    if (threadIdx.x < h)
+      for (int k = 0; k < 3; ++k) part[k][threadIdx.x] += part[k][threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) atomicAdd(&counters[threadIdx.x], part[threadIdx.x][0]);  // passes on two streams
 }
 
 // ---- diagnostics kernels ---------------------------------------------------
@@ -1278,6 +1333,8 @@ struct fr_ctx {
   float* d_mean = nullptr;
   uint8_t* d_u8 = nullptr;
   unsigned long long* d_cnt = nullptr;  // [0..3] counters, [4..] diagnostics; [31] queue head
+  unsigned long long* d_wcnt = nullptr;  // per-wave partial counters (KWork::wave_counters)
+  uint32_t wcnt_waves = 0;               // their capacity in waves
   float* d_samples = nullptr;
   float* d_running = nullptr;
   size_t cap_pixels = 0, cap_samples = 0, cap_running = 0;
@@ -1298,6 +1355,7 @@ struct Grid {
   uint64_t want;  // workgroups the pass could use (items / kBlock)
   int num_cus;
   int* per_cu;    // out: resident workgroups per CU
+  uint32_t* blocks;  // out: workgroups launched
 };
 
 template <typename Kern>
@@ -1313,6 +1371,7 @@ static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t 
   if (const char* e = getenv("FR_MAX_WGS"))
     if (atoi(e) > 0 && static_cast<uint64_t>(atoi(e)) < cap) cap = static_cast<uint64_t>(atoi(e));
   const uint32_t blocks = static_cast<uint32_t>(g.want < cap ? (g.want ? g.want : 1u) : cap);
+  *g.blocks = blocks;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, st, a);
 }
 
@@ -1425,7 +1484,9 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
       hipStreamCreateWithFlags(&c->stream_sum, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream_copy, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming) != hipSuccess ||
-      hipMalloc(&c->d_cnt, 32 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc(&c->d_cnt, 32 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&c->d_wcnt, 2 * 3 * sizeof(unsigned long long) * kMaxWgPerCu * (kBlock / 64u) * c->num_cus) !=
+          hipSuccess) {  // one set per pass slot (traces of consecutive passes overlap)
     fr_ctx_free(c);
     return set_error(FR_EHIP, "fr_ctx_create: event/counter allocation failed");
   }
@@ -1442,6 +1503,7 @@ void fr_ctx_free(fr_ctx* c) {
   if (c->d_mean) (void)hipFree(c->d_mean);
   if (c->d_u8) (void)hipFree(c->d_u8);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
+  if (c->d_wcnt) (void)hipFree(c->d_wcnt);
   if (c->d_samples) (void)hipFree(c->d_samples);
   if (c->d_running) (void)hipFree(c->d_running);
   for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
@@ -1602,6 +1664,9 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
     const unsigned long long z[2] = {0, 0};
     HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fr_diag_lens), z, sizeof(z), 0, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fr_diag_rus), z, sizeof(z), 0, hipMemcpyHostToDevice, c->stream));
+    void* tc = nullptr;
+    HIPCHK(hipGetSymbolAddress(&tc, HIP_SYMBOL(g_fr_tb_cost)));
+    HIPCHK(hipMemsetAsync(tc, 0, (1u << 20) * sizeof(unsigned int), c->stream));
   }
 #endif
   HIPCHK(hipEventRecord(c->ev0, c->stream));
@@ -1625,12 +1690,17 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
       kw.queue = reinterpret_cast<uint32_t*>(c->d_cnt + 31 - slot);
       kw.samples = samples;
       // persistent grid: the resident workgroup count (launch_persistent)
-      const Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy};
+      uint32_t blocks = 0;
+      const Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy, &blocks};
+      unsigned long long* wcnt = c->d_wcnt + static_cast<size_t>(slot) * 3 * kMaxWgPerCu * (kBlock / 64u) * c->num_cus;
+      kw.wave_counters = wcnt;
       HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), ts));
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced], ts));
       launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, grid, lds, ts, ks, kc, kp, kw);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced + 1], ts));
+      hipLaunchKernelGGL(reduce_counters, dim3(1), dim3(256), 0, ts, wcnt, blocks * (kBlock / 64u), c->d_cnt);
+      HIPCHK(hipGetLastError());
       HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_trace[2 * traced + 1], 0));
       ++traced;
     }
@@ -1681,12 +1751,31 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
             cnt[4 + DG_END_L], cnt[4 + DG_UNW_W], cnt[4 + DG_UNW_L], dl[0], dl[1], dr[0], dr[1], cnt[4 + DG_LENS_W],
             cnt[4 + DG_LENS_L], cnt[0], cnt[1], cnt[4 + DG_NODE_W], cnt[4 + DG_NODE_L], cnt[4 + DG_LEAF_W],
             cnt[4 + DG_LEAF_L]);
+    if (const char* path = getenv("FR_DIAG_COST")) {
+      std::vector<unsigned int> tc(1u << 20);
+      HIPCHK(hipMemcpyFromSymbol(tc.data(), HIP_SYMBOL(g_fr_tb_cost), tc.size() * 4));
+      if (FILE* f = fopen(path, "wb")) {
+        fwrite(tc.data(), 4, tc.size(), f);
+        fclose(f);
+      }
+    }
     if (const char* path = getenv("FR_DIAG_TIMES")) {
       std::vector<unsigned long long> wt(2 * 65536);
       HIPCHK(hipMemcpyFromSymbol(wt.data(), HIP_SYMBOL(g_fr_wave_times), wt.size() * 8));
       std::vector<unsigned long long> wd(65536);
       HIPCHK(hipMemcpyFromSymbol(wd.data(), HIP_SYMBOL(g_fr_wave_drain), wd.size() * 8));
       wt.insert(wt.end(), wd.begin(), wd.end());
+      if (const char* pi = getenv("FR_DIAG_ITERS")) {
+        std::vector<unsigned long long> ti(1024 * 1024);
+        HIPCHK(hipMemcpyFromSymbol(ti.data(), HIP_SYMBOL(g_fr_iter_times), ti.size() * 8));
+        if (FILE* f = fopen(pi, "wb")) {
+          fwrite(ti.data(), 8, ti.size(), f);
+          fclose(f);
+        }
+      }
+      std::vector<unsigned int> wi(2 * 65536);
+      HIPCHK(hipMemcpyFromSymbol(wi.data(), HIP_SYMBOL(g_fr_wave_iters), wi.size() * 4));
+      for (size_t k = 0; k < wi.size(); k += 2) wt.push_back((static_cast<unsigned long long>(wi[k + 1]) << 32) | wi[k]);
       if (FILE* f = fopen(path, "wb")) {
         fwrite(wt.data(), 8, wt.size(), f);
         fclose(f);

@@ -23,3 +23,17 @@ for f in [0.5, 0.7, 0.8, 0.85, 0.9, 0.95, 0.98]:
     tt = f * T
     print(f"  t={tt/1e3:.3f} ms ({f:.0%}): {np.mean((s <= tt) & (e > tt)):.1%} of waves running")
 print(f"  wave starts: first {s.min()/1e3:.4f} ms, last {s.max()/1e3:.4f} ms")
+# iterations (appended after the drain stamps: per wave, end << 32 | at first drain)
+if raw.size >= 4 * 65536:
+    it = raw[3 * 65536: 4 * 65536][:n]
+    i_end, i_dr = (it >> np.uint64(32)).astype(np.float64), (it & np.uint64(0xFFFFFFFF)).astype(np.float64)
+    okk = ok & (i_end > 0)
+    rate_all = e[okk] / np.maximum(i_end[okk], 1)
+    rate_tail = (e[okk] - (dr[okk].astype(np.float64) - t0) / 100.0) / np.maximum(i_end[okk] - i_dr[okk], 1)
+    print(f"iterations per wave: mean {i_end[okk].mean():.0f}; after first drain mean {(i_end - i_dr)[okk].mean():.0f} "
+          f"max {(i_end - i_dr)[okk].max():.0f}")
+    print(f"us per iteration: whole kernel mean {rate_all.mean():.2f}; after drain mean {rate_tail.mean():.2f} "
+          f"p10 {np.percentile(rate_tail, 10):.2f} p90 {np.percentile(rate_tail, 90):.2f}")
+    last = np.argsort(e[okk])[-5:]
+    print("last 5 waves: end ms", np.round(e[okk][last] / 1e3, 3), "drain ms",
+          np.round((dr[okk][last].astype(np.float64) - t0) / 1e5, 3), "iters after drain", (i_end - i_dr)[okk][last])
