@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 out="gpurun_out/prof/$tag"
 mkdir -p "$out"
-B="${PROF_CMD:-python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline}"
+B="${PROF_CMD:-python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-pmc}"
 run() {  # name seconds args...
   local name=$1 secs=$2; shift 2
   echo "=== $name"
