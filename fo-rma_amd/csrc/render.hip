@@ -334,8 +334,13 @@ enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 // cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
 // admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
 template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, bool DEFER>
-#ifdef FR_WAVES_PER_EU
-#define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU, FR_WAVES_PER_EU)))
+// FR_MIN_WAVES: at least this many waves per SIMD (6: <= 80 VGPRs); the general (KS_ANY)
+// and BVH kernels otherwise settle at 83-94 VGPRs, 5 waves. 0: no request.
+#ifndef FR_MIN_WAVES
+#define FR_MIN_WAVES 6
+#endif
+#if FR_MIN_WAVES > 0
+#define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(FR_MIN_WAVES)))
 #else
 #define FR_OCC_ATTR
 #endif
@@ -473,9 +478,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         // Every lane of the wave is here: a lane retires only after the queue has
         // drained, and from then on no batch holds a valid item. A slot past the image
         // or the queue gets a stream that is never used.
+#if defined(__HIP_DEVICE_COMPILE__)
+        // the item split's parameters reloaded from the kernarg segment here (once per 64
+        // items) rather than held in SGPRs across the loop, like the camera (step 1)
+        typedef __attribute__((address_space(4))) const KArgs cargs_g;
+        cargs_g* apg = (cargs_g*)(__builtin_amdgcn_kernarg_segment_ptr());
+        asm volatile("" : "+s"(apg));
+        const KParams kg = apg->kp;
+#else
+        const KParams& kg = kp;
+#endif
         uint32_t bb, qq, xx, yy;
-        const bool in_image = item_xy(kp, base + lane, bb, qq, xx, yy);
-        held = rng_seed(kp.seed, yy * kp.W + xx, bb);
+        const bool in_image = item_xy(kg, base + lane, bb, qq, xx, yy);
+        held = rng_seed(kg.seed, yy * kg.W + xx, bb);
         held_xy = in_image ? (xx | (yy << 16)) : 0xFFFFFFFFu;
         held_b = bb;
         if (lane < kBatch - avail) {  // the new batch's first slots are taken now
@@ -485,9 +500,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         }
         // Queue tail: the waves that claim last hold the longest remaining work, so they
         // get issue priority over waves finishing older items (shortens the drain).
-        if (base >= kp.prio_at[0]) {
-          if (base >= kp.prio_at[2]) __builtin_amdgcn_s_setprio(3);
-          else if (base >= kp.prio_at[1]) __builtin_amdgcn_s_setprio(2);
+        if (base >= kg.prio_at[0]) {
+          if (base >= kg.prio_at[2]) __builtin_amdgcn_s_setprio(3);
+          else if (base >= kg.prio_at[1]) __builtin_amdgcn_s_setprio(2);
           else __builtin_amdgcn_s_setprio(1);
         }
       }

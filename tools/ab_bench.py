@@ -18,7 +18,13 @@ import json, os, sys, hashlib
 sys.path.insert(0, os.path.join(sys.argv[1], "fo-rma_amd"))
 import forma_rt as fr
 scene, w, h, spp, depth, steps, shards = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), int(sys.argv[6]), int(sys.argv[7]), int(sys.argv[8])
-sc = fr.Scene.from_file(fr.scene_path(scene), w, h)
+if scene.startswith("gen:"):
+    sys.path.insert(0, os.path.join(sys.argv[1], "tools"))
+    import gen_scene
+    _, count, mesh = scene.split(":")
+    sc = fr.Scene.from_json(gen_scene.dumps(gen_scene.generator_scene(int(count), mesh)), w, h)
+else:
+    sc = fr.Scene.from_file(fr.scene_path(scene), w, h)
 ctx = fr.RenderContext(0)
 p = fr.make_params(w, h, spp, depth, shard_index=0, shard_count=shards)
 ctx.render(sc, sc.camera, p); ctx.sync()
