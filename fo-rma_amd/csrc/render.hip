@@ -334,15 +334,15 @@ enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 // cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
 // admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
 template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, bool DEFER>
-// FR_MIN_WAVES: at least this many waves per SIMD (6: <= 80 VGPRs); the general (KS_ANY)
-// and BVH kernels otherwise settle at 83-94 VGPRs, 5 waves. 0: no request.
-#ifndef FR_MIN_WAVES
-#define FR_MIN_WAVES 6
-#endif
-#if FR_MIN_WAVES > 0
+// Waves per SIMD the kernels ask for: the list-loop kernels at least 7 (<= 72 VGPRs), the
+// BVH kernels at least 6 (<= 80); without the request the general (KS_ANY) and BVH
+// kernels settle at 83-94 VGPRs, 5 waves. Measured (tools/ab_bench.py): 7 for the list
+// kernels (scene_01 C2 37.9 -> 36.0 ms, a few VGPRs spilled to scratch), 6 for the BVH
+// ones (7 or 8 spill more: C5 +2-10 %, scene_06 +12-20 %). FR_MIN_WAVES=n forces n.
+#ifdef FR_MIN_WAVES
 #define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(FR_MIN_WAVES)))
 #else
-#define FR_OCC_ATTR
+#define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(BVH ? 6 : 7)))
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) FR_OCC_ATTR void trace_kernel(
     KArgs args) {
