@@ -86,6 +86,17 @@ constexpr uint32_t KF_DEFER = 1u << 31;            // internal KParams.flags bit
 #define FR_BLOCK_SAMPLES 16  // RNG contract: one stream per 16-sample block (oracle.cpp agrees)
 #endif
 constexpr uint32_t kBlockSamples = FR_BLOCK_SAMPLES;  // samples per RNG stream (numerics contract)
+// The last block of a pixel with more than one block is split into sub-blocks of
+// kFineSamples samples, each its own stream (key kFineKey | s / kFineSamples): the queue
+// ends with short items, so the drain after the last claim is short.
+#ifndef FR_FINE_SAMPLES
+#define FR_FINE_SAMPLES 4
+#endif
+constexpr uint32_t kFineSamples = FR_FINE_SAMPLES;
+constexpr uint32_t kFineSub = kBlockSamples / kFineSamples;  // sub-blocks per block
+constexpr uint32_t kFineKey = 0x80000000u;
+static_assert(kFineSamples >= 1 && kBlockSamples % kFineSamples == 0 && kFineSub <= 4,
+              "sub-block index packs into 2 bits of the claim's block word");
 // work items reserved per step of the global counter: one tile of one sample block,
 // seeded by the wave's 64 lanes at once (trace_kernel's claim step)
 constexpr uint32_t kBatch = 64;
@@ -142,6 +153,10 @@ struct KParams {
   uint32_t band_h;                    // FR_FLAG_MT_BANDS: rows per band, H / 4 (tracer.rs:87)
   uint32_t prio_at[3];  // a wave reserving a batch at or past prio_at[k] raises its priority to k + 1
   uint32_t ks;          // sample slots per work item in the sample buffer: min(spp, kBlockSamples)
+  // items [n_coarse, n_items) are the sub-blocks of block b_fine (the pixels' last block,
+  // when spp > kBlockSamples and this pass holds it): item = n_coarse + k * P + q for
+  // sub-block k; n_coarse = n_items when the pass has none
+  uint32_t n_coarse, b_fine;
 };
 
 // Unsigned 32-bit division by the invariant n_tiles: q = (t + ((x - t) >> s1)) >> s2 with
@@ -240,6 +255,8 @@ constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for smal
 #define FR_STAGE 4  // 1 or 4 (A/B builds)
 #endif
 __host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? 1u : FR_STAGE; }
+// a sub-block starts on a staging group: the group's store covers only its own samples
+static_assert(kFineSamples % FR_STAGE == 0, "sub-blocks hold whole staging groups");
 
 // FR_DIAG builds count, per phase, wave-level trips (one per SIMT pass of the wave)
 // and lane-level work, to measure SIMT efficiency. Never enabled in the product.
@@ -294,15 +311,24 @@ __device__ __forceinline__ bool slot_xy(const KParams& kp, uint32_t q, uint32_t&
   return x < kp.W && y < kp.H;
 }
 
-// Work item -> (block b, pixel slot q, image x, y); false for a slot past the image edge.
-// item = (b - b0) * P + q with P = 64 * n_tiles: split via the tile-block index.
-__device__ __forceinline__ bool item_xy(const KParams& kp, uint32_t item, uint32_t& b, uint32_t& q, uint32_t& x,
+// Work item -> (block word bw, pixel slot q, image x, y); false for a slot past the image
+// edge. item = (b - b0) * P + q with P = 64 * n_tiles (split via the tile-block index),
+// or n_coarse + k * P + q for sub-block k of block b_fine. bw = b for a whole block,
+// b | kFineKey | k << 28 for a sub-block (b < 2^28: spp < 2^32).
+__device__ __forceinline__ bool item_xy(const KParams& kp, uint32_t item, uint32_t& bw, uint32_t& q, uint32_t& x,
                                         uint32_t& y) {
-  const uint32_t tb = item >> 6;
+  const bool fine = item >= kp.n_coarse;
+  const uint32_t tb = (fine ? item - kp.n_coarse : item) >> 6;  // n_coarse is a multiple of 64
   const uint32_t bl = fastdiv(tb, kp.tiles_magic, kp.tiles_shift);
-  b = kp.b0 + bl;
+  bw = fine ? (kp.b_fine | kFineKey | (bl << 28)) : kp.b0 + bl;
   q = ((tb - bl * kp.n_tiles) << 6) | (item & 63u);
   return slot_xy(kp, q, x, y);
+}
+
+// RNG stream key of a block word: the block index, or kFineKey | s / kFineSamples for a
+// sub-block starting at sample s (oracle.cpp stream_key agrees)
+__host__ __device__ __forceinline__ uint32_t stream_key(uint32_t bw) {
+  return (bw & kFineKey) ? (kFineKey | ((bw & 0x0FFFFFFFu) * kFineSub + ((bw >> 28) & 3u))) : bw;
 }
 
 // Persistent path-tracing kernel. Work item = (pixel slot q, sample block b): the
@@ -490,7 +516,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #endif
         uint32_t bb, qq, xx, yy;
         const bool in_image = item_xy(kg, base + lane, bb, qq, xx, yy);
-        held = rng_seed(kg.seed, yy * kg.W + xx, bb);
+        held = rng_seed(kg.seed, yy * kg.W + xx, stream_key(bb));
         held_xy = in_image ? (xx | (yy << 16)) : 0xFFFFFFFFu;
         held_b = bb;
         if (lane < kBatch - avail) {  // the new batch's first slots are taken now
@@ -543,15 +569,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           vofs = static_cast<float>(3u - k) * 0.25f;
         }
         if (ok) {
-          rng = st;  // this block's stream: rng_seed(seed, y * W + x, b)
-          s = b * kBlockSamples;
-          out = kw.samples + 3 * (static_cast<size_t>(item) * kp.ks);
-          jj = 0;
+          rng = st;  // this item's stream: rng_seed(seed, y * W + x, stream_key(b))
+          // a sub-block k of block b_fine: samples [16 b + 4 k, +4) of the block's slot
+          // (item - k * P in the buffer); a whole block: k = 0
+          const uint32_t k = (b >> 28) & 3u;
+          const bool fine = (b & kFineKey) != 0u;
+          jj = k * kFineSamples;
+          s = (b & 0x0FFFFFFFu) * kBlockSamples + jj;
+          out = kw.samples + 3 * (static_cast<size_t>(item - k * kp.P) * kp.ks);
 #ifdef FR_DIAG
           diag_tb = item >> 6;
           diag_seg0 = nseg;
 #endif
-          s_end = min(s + kBlockSamples, kp.spp);
+          s_end = min(s + (fine ? kFineSamples : kBlockSamples), kp.spp);
           fx = static_cast<float>(x);
           fy = static_cast<float>(yrow);
           need_jit = true;
@@ -1619,8 +1649,14 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   // once per lane (each claim retires >= 1 lane): <= 8 blocks/CU x 4 waves x 64 x 64 on
   // 256 CUs = 2^25 past n_items, so keep 2^28 of headroom below 2^32.
   constexpr uint32_t kItemLimit = 0xFFFFFFFFu - (1u << 28);
+  // The pass holding the last block runs its kFineSub sub-blocks as items: up to
+  // (nb + kFineSub - 1) x P items.
+  const uint32_t fine_extra = nblocks > 1 ? kFineSub - 1u : 0u;
+  if (kp.P && kItemLimit / kp.P < 1u + fine_extra)
+    return set_error(FR_EARG, "shard of %u pixel slots exceeds the 32-bit work-item range at spp %u; use more shards",
+                     kp.P, p->spp);
   uint32_t nb_max = static_cast<uint32_t>(passes_u > 1 ? cap_blocks / 2 : cap_blocks);
-  if (kp.P && nb_max > kItemLimit / kp.P) nb_max = kItemLimit / kp.P;
+  if (kp.P && nb_max > kItemLimit / kp.P - fine_extra) nb_max = kItemLimit / kp.P - fine_extra;
   if (nb_max < 1) nb_max = 1;
   if (nb_pass > nb_max) {
     nb_pass = nb_max;
@@ -1698,6 +1734,15 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
     kp.b0 = static_cast<uint32_t>(pass) * nb_pass;
     kp.nb = pass < passes ? min(nb_pass, nblocks - kp.b0) : 0u;
     kp.n_items = kp.nb * kp.P;
+    kp.n_coarse = kp.n_items;
+    kp.b_fine = 0;
+    if (kFineSub > 1 && nblocks > 1 && kp.nb && kp.b0 + kp.nb == nblocks) {
+      // the pixels' last block, as sub-blocks of kFineSamples: the queue's last items
+      const uint32_t n_last = p->spp - (nblocks - 1u) * kBlockSamples;
+      kp.n_coarse = (kp.nb - 1u) * kp.P;
+      kp.b_fine = nblocks - 1u;
+      kp.n_items = kp.n_coarse + ((n_last + kFineSamples - 1u) / kFineSamples) * kp.P;
+    }
     for (int k = 0; k < 3; ++k)
       kp.prio_at[k] = tail_prio ? kp.n_items - kp.n_items / (tail_prio << (2 * k)) : 0xFFFFFFFFu;
     if (kp.n_items) {

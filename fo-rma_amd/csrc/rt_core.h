@@ -65,11 +65,12 @@ FR_HD float schlick(float cosine, float ref_idx) {
 }
 
 // ---------------------------------------------------------------------------
-// RNG. One stream per (seed, pixel, block of 16 samples): splitmix64 keys a
-// xoshiro128+ 1.0 state (Blackman & Vigna's generator for floating-point output:
-// only the upper bits are used); a block's samples draw from it in sample order (the
-// reference's save_image draws every sample from one sequential stream,
-// tracer.rs:164-175). f32 = ((u32 ^ 2^31) >> 8) * 2^-24 (24 random bits).
+// RNG. One stream per (seed, pixel, key): key b for block b of 16 samples, and, when
+// spp > 16, 2^31 | s / 4 for the 4-sample sub-blocks of the pixel's last block
+// (render.hip stream_key). splitmix64 keys a xoshiro128+ 1.0 state (Blackman & Vigna's
+// generator for floating-point output: only the upper bits are used); a stream's
+// samples draw from it in sample order (the reference's save_image draws every sample
+// from one sequential stream, tracer.rs:164-175). f32 = ((u32 ^ 2^31) >> 8) * 2^-24.
 // ---------------------------------------------------------------------------
 struct Rng {
   uint32_t s0, s1, s2, s3;

@@ -75,9 +75,9 @@ struct ReflectRecord {
 
 // ---- the RNG that replaces rand::thread_rng() -------------------------------
 // splitmix64 (Steele, Lea & Flood 2014) keys xoshiro128+ 1.0 (Blackman & Vigna
-// 2018) per (seed, pixel, stream); sample s of a pixel draws from stream s / 16, the
-// 16 samples of a block in order (the reference's save_image draws every sample from
-// one sequential ThreadRng, tracer.rs:164-175); f32 = ((u32 ^ 2^31) >> 8) * 2^-24.
+// 2018) per (seed, pixel, stream key); a pixel's samples draw from their streams in
+// order (stream_start below; the reference's save_image draws every sample from one
+// sequential ThreadRng, tracer.rs:164-175); f32 = ((u32 ^ 2^31) >> 8) * 2^-24.
 struct Rng {
   uint32_t s[4];
   static uint64_t splitmix(uint64_t& x) {
@@ -109,6 +109,22 @@ struct Rng {
   }
   float gen_f32() { return float((next_u32() ^ 0x80000000u) >> 8) * (1.0f / 16777216.0f); }
 };
+
+// Stream layout of one pixel's spp samples: blocks of 16 consecutive samples, block b
+// drawing from stream key b; when spp > 16, the last block (the one holding sample
+// spp - 1) is split into sub-blocks of 4 samples, the one starting at sample s drawing
+// from stream key 2^31 | s / 4. True when sample s starts a stream, with its key.
+bool stream_start(uint32_t s, uint32_t spp, uint32_t& key) {
+  const uint32_t last_block = (spp - 1) / 16;
+  if (spp > 16 && s / 16 == last_block) {
+    if (s % 4 != 0) return false;
+    key = 0x80000000u | (s / 4);
+    return true;
+  }
+  if (s % 16 != 0) return false;
+  key = s / 16;
+  return true;
+}
 
 // ---- cpu_ray_tracer/utility.rs ---------------------------------------------
 Vec3 random_in_unit_circle(Rng& rng) {  // :4-13
@@ -753,8 +769,9 @@ int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, ui
         Vec3 col = Vec3::zero();
         Rng rng(seed, pixel, 0);
         for (uint32_t s = 0; s < spp; ++s) {
-          // samples come in blocks of 16; block b draws from stream (seed, pixel, b) in order
-          if (s % 16 == 0) rng = Rng(seed, pixel, s / 16);
+          // samples come in streams of 16 (4 in the last block); each draws in order
+          uint32_t key;
+          if (stream_start(s, spp, key)) rng = Rng(seed, pixel, key);
           const float u = (float(x) + rng.gen_f32()) / float(width);
           const float v = (float(height - y) + rng.gen_f32()) / float(height);
           const Ray ray = camera.get_ray(u, v, rng);
@@ -798,7 +815,7 @@ int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, ui
 // v = ((t_height - y) + r) / H + t_id * 0.25, gamma-corrects and quantises every pixel
 // to u8, and the passes are averaged as acc += u8 / sample in f32, then `as u8`. Rows
 // past 4 * t_height are never written (0). A pixel's passes draw from the build's
-// streams exactly as save_image's samples do (block s / 16 of (seed, pixel)), so the
+// streams exactly as save_image's samples do (stream_start of (seed, pixel)), so the
 // per-pixel stream state is carried from pass to pass.
 int oracle_render_mt(const or_prim* prims, uint32_t n, const or_camera* cam, uint32_t width, uint32_t height,
                      uint32_t sample, uint32_t max_depth, uint64_t seed, float* out_acc, uint8_t* out_u8,
@@ -821,7 +838,8 @@ int oracle_render_mt(const or_prim* prims, uint32_t n, const or_camera* cam, uin
           const uint32_t row = (NTHREADS - 1 - t_id) * t_height + y;  // ids sorted descending (:122-127)
           const uint32_t pixel = row * width + x;
           Rng& rng = streams[pixel];
-          if (pass % 16 == 0) rng = Rng(seed, pixel, pass / 16);
+          uint32_t key;
+          if (stream_start(pass, sample, key)) rng = Rng(seed, pixel, key);
           const float u = (float(x) + rng.gen_f32()) / float(width);
           float v = (float(t_height - y) + rng.gen_f32()) / float(height);
           v += float(t_id) * t_offset;

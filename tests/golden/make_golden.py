@@ -32,6 +32,8 @@ CASES = {
     "scene02_mesh_48x27_s3_d8": ("json:scene_02", 48, 27, 3, 8, 0x5EED),
     "scene06_cyl_48x27_s2_d8": ("json:scene_06", 48, 27, 2, 8, 0x5EED),
     "scene09_tet_40x40_s4_d8": ("json:scene_09", 40, 40, 4, 8, 0x5EED),
+    # 37 spp: two 16-sample streams, then the last block as sub-block streams of 4, 1
+    "scene08_24x16_s37_d8": ("json:scene_08", 24, 16, 37, 8, 0x5EED),
 }
 
 

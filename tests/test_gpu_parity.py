@@ -299,6 +299,20 @@ def test_edge_cases(gpu, case):
     assert_parity(mean, u8, st, omean, ou8, ocnt)
 
 
+@pytest.mark.parametrize("spp", [16, 17, 20, 21, 32, 33, 47, 48])
+def test_last_block_sub_block_streams(gpu, spp):
+    """Around the stream layout's edges: spp = 16 (one block, no sub-blocks), a last block
+    of 1, 4, 5, 15 or 16 samples (sub-blocks of 4, the last partial); the sub-block items
+    are the queue's last items and land in their block's sample slots."""
+    w, h, depth = 40, 24, 8
+    sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth, seed=spp)
+    prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path("scene_08")).read())
+    cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
+    omean, ou8, ocnt, _ = O.render(prims, cam, w, h, spp, depth, seed=spp, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+
+
 @pytest.mark.parametrize("wgs,scene,w,h,spp,depth", [(1, "scene_08", 64, 40, 40, 8), (3, "scene_01", 48, 32, 20, 8),
                                                     (1, "scene_02", 40, 24, 3, 12), (2, "scene_08", 72, 16, 1, 4)])
 def test_small_grid_claims_many_batches(gpu, wgs, scene, w, h, spp, depth, monkeypatch):

@@ -2,6 +2,7 @@
 # Build libforma_rt from the kernel sources of a git revision, for A/B timing against the
 # working tree (tools/ab_bench.py):
 #   tools/build_ref_variant.sh REV NAME [DEFS]  ->  fo-rma_amd/build/variants/libforma_rt_NAME.so
+# REV "." takes the working tree's sources (for -D variants of uncommitted code).
 # The host objects (scene, JSON, BVH, post) come from the working tree's build; the ABI of
 # REV must match the working tree's include/forma_rt.h.
 set -e
@@ -10,7 +11,11 @@ root="$(cd "$(dirname "$0")/.." && pwd)"
 tmp=$(mktemp -d)
 trap 'rm -rf "$tmp"' EXIT
 mkdir -p "$tmp/fo-rma_amd/csrc" "$tmp/include"
-git -C "$root" archive "$rev" fo-rma_amd/csrc include | tar -x -C "$tmp"
+if [ "$rev" = "." ]; then
+  cp -r "$root/fo-rma_amd/csrc" "$tmp/fo-rma_amd/" && cp -r "$root/include" "$tmp/"
+else
+  git -C "$root" archive "$rev" fo-rma_amd/csrc include | tar -x -C "$tmp"
+fi
 make -C "$root/fo-rma_amd" -s build/scene.o build/json_min.o build/bvh.o build/post.o
 mkdir -p "$root/fo-rma_amd/build/variants"
 FP="-ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero"
