@@ -647,10 +647,11 @@ def test_pass_pipeline_never_changes_results(gpu, pipe, buf_gb, monkeypatch):
 
 
 @pytest.mark.slow
-def test_c4_shard_on_row_subset(gpu):
+def test_c4_shard_on_row_subset(gpu, monkeypatch):
     """C4 (scene_08 3840x2160, 1024 spp, 8 bounces) as one of 8 ranks renders it: shard 0
-    of 8 (8-row strips 0, 8, 16, ...), checked on a subset of that shard's rows. The
-    render runs in passes (the sample buffer holds 21 of its 64 blocks)."""
+    of 8 (8-row strips 0, 8, 16, ...), checked on a subset of that shard's rows. With an
+    8-GB sample buffer the render runs in passes (the buffer holds 21 of its 64 blocks)."""
+    monkeypatch.setenv("FR_SAMPLE_BUFFER_GB", "8")
     w, h, spp, depth = 3840, 2160, 1024, 8
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
     mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth, shard_index=0, shard_count=8)
