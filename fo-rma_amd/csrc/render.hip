@@ -155,6 +155,9 @@ struct KParams {
   uint32_t band_h;                    // FR_FLAG_MT_BANDS: rows per band, H / 4 (tracer.rs:87)
   uint32_t prio_at[3];  // a wave reserving a batch at or past prio_at[k] raises its priority to k + 1
   uint32_t ks;          // sample slots per work item in the sample buffer: min(spp, kBlockSamples)
+  // items handed out without the queue: wave w of the grid starts on batch w (one batch
+  // per wave, n_static = waves x 64); the queue counts from n_static
+  uint32_t n_static;
   // items [n_coarse, n_items) are the sub-blocks of block b_fine (the pixels' last block,
   // when spp > kBlockSamples and this pass holds it): item = n_coarse + k * P + q for
   // sub-block k; n_coarse = n_items when the pass has none
@@ -476,6 +479,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // ... and the same slot's pixel (x | y << 16, all ones past the image edge) and sample
   // block, so a claiming lane fetches those by permute too instead of dividing the item
   uint32_t held_xy = 0xFFFFFFFFu, held_b = 0u;
+  // A wave's first batch is its own (wave w of the grid: batch w), seeded here: 7168
+  // first claims at once on one counter would queue for ~80 us (about 88 returning
+  // atomics per us on one word, MI355X_MICROARCH.md "dequeue").
+  {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(4))) const KArgs cargs_0;
+    cargs_0* ap0 = (cargs_0*)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(ap0));
+    const KParams k0 = ap0->kp;
+#else
+    const KParams& k0 = kp;
+#endif
+    q_next = (blockIdx.x * (kBlock / 64u) + (tid >> 6)) * kBatch;
+    q_end = q_next + kBatch;
+    uint32_t bb, qq, xx, yy;
+    const bool in_image = item_xy(k0, q_next + lane, bb, qq, xx, yy);
+    held = rng_seed(k0.seed, yy * k0.W + xx, stream_key(bb));
+    held_xy = in_image ? (xx | (yy << 16)) : 0xFFFFFFFFu;
+    held_b = bb;
+  }
   while (active) {
     DIAG_WAVE(DG_ITER);
 #ifdef FR_DIAG
@@ -502,7 +525,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       if (grab) {
         if (static_cast<int>(lane) == first) base = atomicAdd(kw.queue, kBatch);
         base = __builtin_amdgcn_readlane(base, first);
-        q_end = base + kBatch;
         // Every lane of the wave is here: a lane retires only after the queue has
         // drained, and from then on no batch holds a valid item. A slot past the image
         // or the queue gets a stream that is never used.
@@ -516,6 +538,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #else
         const KParams& kg = kp;
 #endif
+        base += kg.n_static;  // past the waves' first batches
+        q_end = base + kBatch;
         uint32_t bb, qq, xx, yy;
         const bool in_image = item_xy(kg, base + lane, bb, qq, xx, yy);
         held = rng_seed(kg.seed, yy * kg.W + xx, stream_key(bb));
@@ -1407,7 +1431,7 @@ struct Grid {
 };
 
 template <typename Kern>
-static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t st, const KArgs& a) {
+static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t st, KArgs a) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, static_cast<int>(kBlock), lds) != hipSuccess ||
       per_cu < 1)
@@ -1420,6 +1444,7 @@ static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t 
     if (atoi(e) > 0 && static_cast<uint64_t>(atoi(e)) < cap) cap = static_cast<uint64_t>(atoi(e));
   const uint32_t blocks = static_cast<uint32_t>(g.want < cap ? (g.want ? g.want : 1u) : cap);
   *g.blocks = blocks;
+  a.kp.n_static = blocks * kBlock;  // one 64-item batch per wave of the grid
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, st, a);
 }
 
