@@ -301,7 +301,13 @@ enum { PF_CLAIM, PF_REJ, PF_HIT, PF_SHADE, PF_END, PF_N };
 
 // HAS_PLANE: planes may leave the shared record's t/p stale (plane.rs:27-29), so
 // the last written t is tracked separately from the winner's.
-__device__ __forceinline__ uint32_t lanes_set(bool b) { return static_cast<uint32_t>(__popcll(__ballot(b))); }
+// (two 32-bit popcounts: a 64-bit one leaves a 64-bit count whose compare the SALU
+// cannot do, and the compiler moved it to the VALU)
+__device__ __forceinline__ uint32_t lanes_set(bool b) {
+  const unsigned long long m = __ballot(b);
+  return static_cast<uint32_t>(__builtin_popcount(static_cast<uint32_t>(m)) +
+                               __builtin_popcount(static_cast<uint32_t>(m >> 32)));
+}
 
 // Pixel slot q of a shard -> image coordinates. Slots run tile by tile (8x8 pixels,
 // tiles left to right within an 8-row strip, the shard's strips top to bottom); slots
@@ -520,14 +526,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       uint32_t base = 0;
       const bool grab = n > avail;
       const int first = __ffsll(static_cast<long long>(m)) - 1;
-      Rng src = held;  // slots [64 - avail, 64) still hold the current batch's streams
-      uint32_t src_xy = held_xy, src_b = held_b;
+      // The item's stream start, pixel and block, by lane permute from the lane that
+      // seeded them: first from the current batch (claims r < avail), then, after a grab,
+      // from the new batch (claims r >= avail). Every lane of the wave is active at both
+      // permutes (a permute reads 0 from an inactive source): a lane retires only after
+      // the queue has drained, and from then on no batch holds a valid item.
+      int sl = static_cast<int>(((next + r) & (kBatch - 1u)) << 2);
+      Rng st{static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s0))),
+             static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s1))),
+             static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s2))),
+             static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s3)))};
+      uint32_t xy = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_xy)));
+      uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_b)));
       if (grab) {
         if (static_cast<int>(lane) == first) base = atomicAdd(kw.queue, kBatch);
         base = __builtin_amdgcn_readlane(base, first);
-        // Every lane of the wave is here: a lane retires only after the queue has
-        // drained, and from then on no batch holds a valid item. A slot past the image
-        // or the queue gets a stream that is never used.
+        // A slot past the image or the queue gets a stream that is never used.
 #if defined(__HIP_DEVICE_COMPILE__)
         // the item split's parameters reloaded from the kernarg segment here (once per 64
         // items) rather than held in SGPRs across the loop, like the camera (step 1)
@@ -545,10 +559,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         held = rng_seed(kg.seed, yy * kg.W + xx, stream_key(bb));
         held_xy = in_image ? (xx | (yy << 16)) : 0xFFFFFFFFu;
         held_b = bb;
-        if (lane < kBatch - avail) {  // the new batch's first slots are taken now
-          src = held;
-          src_xy = held_xy;
-          src_b = held_b;
+        // claims r >= avail take the new batch's slots r - avail (base is a multiple of 64)
+        sl = static_cast<int>(((r - avail) & (kBatch - 1u)) << 2);
+        const Rng st2{static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s0))),
+                      static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s1))),
+                      static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s2))),
+                      static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s3)))};
+        const uint32_t xy2 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_xy)));
+        const uint32_t b2 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_b)));
+        if (r >= avail) {
+          st = st2;
+          xy = xy2;
+          b = b2;
         }
         // Queue tail: the waves that claim last hold the longest remaining work, so they
         // get issue priority over waves finishing older items (shortens the drain).
@@ -560,15 +582,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       }
       q_next = grab ? base + (n - avail) : next + n;
       const uint32_t item = r < avail ? next + r : base + (r - avail);
-      // the item's stream start, from the lane that seeded it (before any lane retires)
-      const int sl = static_cast<int>((item & (kBatch - 1u)) << 2);
-      const Rng st{static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s0))),
-                   static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s1))),
-                   static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s2))),
-                   static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src.s3)))};
-      // (every lane of the wave is active here: a permute reads 0 from an inactive source)
-      const uint32_t xy = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src_xy)));
-      const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(src_b)));
       if (need_item && item >= kp.n_items) {
 #ifdef FR_DIAG
         if (gw < 65536) {
@@ -643,7 +656,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           // the test in the 2^23-scaled domain (rng_signed_unit_scaled): same decisions
           px = rng_signed_unit_scaled(rng);
           py = rng_signed_unit_scaled(rng);
-          pz = sph ? rng_signed_unit_scaled(rng) : 0.0f;
+          if (sph) pz = rng_signed_unit_scaled(rng);  // a circle try keeps pz = 0
           acc = !(px * px + py * py + pz * pz >= kUnitBallScaled);
         }
       } while (lanes_set(!acc) > static_cast<uint32_t>(KREJ));
