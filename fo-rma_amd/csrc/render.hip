@@ -82,6 +82,7 @@ constexpr uint32_t kDeferMaxPrims = 254;
 constexpr uint32_t kDeferUnit = 255;
 constexpr uint32_t kDeferAbsorbed = 0xBF800000u;  // -1.0f
 constexpr uint32_t KF_DEFER = 1u << 31;            // internal KParams.flags bit: records, not colours
+constexpr uint32_t KF_STAGE = 1u << 30;            // internal: BVH kernel stages its samples in LDS
 #ifndef FR_BLOCK_SAMPLES
 #define FR_BLOCK_SAMPLES 16  // RNG contract: one stream per 16-sample block (oracle.cpp agrees)
 #endif
@@ -259,7 +260,13 @@ constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for smal
 #ifndef FR_STAGE
 #define FR_STAGE 4  // 1 or 4 (A/B builds)
 #endif
-__host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? 1u : FR_STAGE; }
+// The BVH kernels stage 2 samples when the 6 KB this adds to their LDS (which holds the
+// traversal stack) keeps their resident workgroups per CU (KF_STAGE, decided at launch):
+// C5 66.8 -> 64.3 ms; on scenes whose LDS tables fill the CU it would cost a workgroup.
+#ifndef FR_BVH_STAGE
+#define FR_BVH_STAGE 2
+#endif
+__host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? FR_BVH_STAGE : FR_STAGE; }
 // a sub-block starts on a staging group: the group's store covers only its own samples
 static_assert(kFineSamples % FR_STAGE == 0, "sub-blocks hold whole staging groups");
 
@@ -395,11 +402,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // [STG > 1: kBlock x STG staged sample colours (12 B each), lane-major] in front.
   extern __shared__ uint32_t lds[];
   constexpr uint32_t STG = stage_samples(BVH);
+  // list kernels always stage; BVH kernels when the launch gave them the LDS (KF_STAGE)
+  const bool staged = STG > 1 && (!BVH || (kp.flags & KF_STAGE) != 0u);
   float* stage = reinterpret_cast<float*>(lds) + threadIdx.x * (3u * STG);
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
   const uint32_t n_att_st = n_att ? n_att + 1u : 0u;  // with the unit entry
   const uint32_t n_rec = sc.n <= kRecLds ? sc.n : 0u;
-  float4* att_lds = reinterpret_cast<float4*>(lds + (STG > 1 ? kBlock * 3u * STG : 0u));
+  float4* att_lds = reinterpret_cast<float4*>(lds + (staged ? kBlock * 3u * STG : 0u));
   float4* rec_lds = att_lds + n_att_st;
   uint32_t* stack = reinterpret_cast<uint32_t*>(rec_lds + 4u * n_rec);
   uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
@@ -981,7 +990,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           for (int j = udepth - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
         }
       }
-      if (STG == 1) {
+      if (!staged) {
         out[3 * jj] = col.x;
         out[3 * jj + 1] = col.y;
         out[3 * jj + 2] = col.z;
@@ -995,10 +1004,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         if (full || s + 1u == s_end) {
           float* dst = out + 3u * (jj & ~(STG - 1u));
           if (full && kp.ks == kBlockSamples) {
-            // 16-B aligned: item * 192 B + a multiple of 48 B
-            const float4* src = reinterpret_cast<const float4*>(stage);
+            if constexpr ((3u * STG) % 4u == 0u) {
+              // 16-B aligned: item * 192 B + a multiple of 48 B
+              const float4* src = reinterpret_cast<const float4*>(stage);
 #pragma unroll
-            for (uint32_t k = 0; k < 3u * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
+              for (uint32_t k = 0; k < 3u * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
+            } else {
+              // 8-B aligned: item * 192 B + a multiple of 24 B
+              const float2* src = reinterpret_cast<const float2*>(stage);
+#pragma unroll
+              for (uint32_t k = 0; k < 3u * STG / 2u; ++k) reinterpret_cast<float2*>(dst)[k] = src[k];
+            }
           } else {
             for (uint32_t k = 0; k < 3u * ((jj & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
           }
@@ -1441,6 +1457,7 @@ struct Grid {
   int num_cus;
   int* per_cu;    // out: resident workgroups per CU
   uint32_t* blocks;  // out: workgroups launched
+  size_t stage_bytes;  // BVH kernels: LDS for sample staging, taken if it costs no residency
 };
 
 template <typename Kern>
@@ -1449,6 +1466,16 @@ static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t 
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, static_cast<int>(kBlock), lds) != hipSuccess ||
       per_cu < 1)
     per_cu = 1;
+  const char* no_stage = getenv("FR_BVH_STAGE");  // "0": BVH kernels store unstaged (A/B, tests)
+  if (g.stage_bytes && !(no_stage && strcmp(no_stage, "0") == 0)) {
+    int staged = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&staged, kern, static_cast<int>(kBlock), lds + g.stage_bytes) ==
+            hipSuccess &&
+        staged >= per_cu) {
+      lds += g.stage_bytes;
+      a.kp.flags |= KF_STAGE;
+    }
+  }
   *g.per_cu = per_cu;
   uint64_t cap = static_cast<uint64_t>(per_cu) * static_cast<uint64_t>(g.num_cus);
   // FR_MAX_WGS=k caps the grid (tests: with a few workgroups every wave claims many
@@ -1751,7 +1778,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
                                                sizeof(uint32_t);
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
   const size_t stage_n = stage_samples(use_bvh);
-  const size_t lds = (stage_n > 1 ? kBlock * stage_n * 3 * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
+  const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * 3 * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
                      n_rec * 64 + stack_bytes + (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
   KWork kw;
   kw.counters = c->d_cnt;
@@ -1798,7 +1825,8 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
       kw.samples = samples;
       // persistent grid: the resident workgroup count (launch_persistent)
       uint32_t blocks = 0;
-      const Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy, &blocks};
+      const Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy, &blocks,
+                      use_bvh && stage_n > 1 ? kBlock * stage_n * 3 * sizeof(float) : 0u};
       unsigned long long* wcnt = c->d_wcnt + static_cast<size_t>(slot) * 3 * kMaxWgPerCu * (kBlock / 64u) * c->num_cus;
       kw.wave_counters = wcnt;
       HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), ts));
