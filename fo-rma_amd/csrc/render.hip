@@ -83,6 +83,12 @@ constexpr uint32_t kDeferUnit = 255;
 constexpr uint32_t kDeferAbsorbed = 0xBF800000u;  // -1.0f
 constexpr uint32_t KF_DEFER = 1u << 31;            // internal KParams.flags bit: records, not colours
 constexpr uint32_t KF_STAGE = 1u << 30;            // internal: BVH kernel stages its samples in LDS
+// Scenes of <= kNibbleMaxPrims primitives (the headline scene_08 has 6) keep the winners
+// as 4-bit entries in one register instead of an LDS stack (15 = empty level) and store
+// 8-B records {t, winners}: 2 words per sample instead of 3 (KF_NIBBLE, DEFER == 2).
+constexpr uint32_t kNibbleMaxPrims = 15;
+constexpr uint32_t kNibbleUnit = 15;
+constexpr uint32_t KF_NIBBLE = 1u << 29;           // internal: 8-B deferred records
 #ifndef FR_BLOCK_SAMPLES
 #define FR_BLOCK_SAMPLES 16  // RNG contract: one stream per 16-sample block (oracle.cpp agrees)
 #endif
@@ -377,7 +383,7 @@ enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 // amdgpu_num_sgpr caps the scalar registers (MI355X_MICROARCH.md "Residency and
 // cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
 // admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
-template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, bool DEFER>
+template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, int DEFER>
 // Waves per SIMD the kernels ask for: the list-loop kernels at least 7 (<= 72 VGPRs), the
 // BVH kernels at least 6 (<= 80); without the request the general (KS_ANY) and BVH
 // kernels settle at 83-94 VGPRs, 5 waves. Measured (tools/ab_bench.py): 7 for the list
@@ -402,13 +408,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // [STG > 1: kBlock x STG staged sample colours (12 B each), lane-major] in front.
   extern __shared__ uint32_t lds[];
   constexpr uint32_t STG = stage_samples(BVH);
+  constexpr bool NIB = DEFER == 2;             // 8-B records, winners in a register
+  constexpr uint32_t WPS = NIB ? 2u : 3u;      // words per sample in the buffer
   // list kernels always stage; BVH kernels when the launch gave them the LDS (KF_STAGE)
   const bool staged = STG > 1 && (!BVH || (kp.flags & KF_STAGE) != 0u);
-  float* stage = reinterpret_cast<float*>(lds) + threadIdx.x * (3u * STG);
+  float* stage = reinterpret_cast<float*>(lds) + threadIdx.x * (WPS * STG);
   const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
   const uint32_t n_att_st = n_att ? n_att + 1u : 0u;  // with the unit entry
   const uint32_t n_rec = sc.n <= kRecLds ? sc.n : 0u;
-  float4* att_lds = reinterpret_cast<float4*>(lds + (staged ? kBlock * 3u * STG : 0u));
+  float4* att_lds = reinterpret_cast<float4*>(lds + (staged ? kBlock * WPS * STG : 0u));
   float4* rec_lds = att_lds + n_att_st;
   uint32_t* stack = reinterpret_cast<uint32_t*>(rec_lds + 4u * n_rec);
   uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
@@ -427,9 +435,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   const uint32_t ent_shift = n_att ? 4u : 0u;
   const uint32_t unit_ent = sc.n << ent_shift;
   const uint32_t unit2 = unit_ent | (unit_ent << 16);  // two empty levels
-  if (DEFER)
+  if (DEFER == 1)
     *drow = make_uint2(~0u, ~0u);
-  else if (MAXD > 0)
+  else if (!DEFER && MAXD > 0)
     *hrow = make_uint4(unit2, unit2, unit2, unit2);
   for (uint32_t i = tid; i < n_att_st; i += kBlock) {
     const float4 a = sc.att[i];
@@ -452,9 +460,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 
   enum : uint32_t { NEED_NONE = 0, NEED_LENS = 1, NEED_SPHERE = 2 };
   uint32_t depth = 0;
+  uint32_t wnib = ~0u;  // NIB: the winners, level k in bits 4k..4k+3 (15: empty)
   // stack push at level `depth` of the scatter winner
   auto push = [&](uint32_t pi) {
-    if (DEFER)
+    if (NIB)
+      wnib ^= (pi ^ kNibbleUnit) << (4u * depth);
+    else if (DEFER)
       bstack[tid * 8u + depth] = static_cast<uint8_t>(pi);
     else if (MAXD > 0)
       hstack[tid * MAXD + depth] = static_cast<uint16_t>(pi << ent_shift);
@@ -624,7 +635,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           const bool fine = (b & kFineKey) != 0u;
           jj = k * kFineSamples;
           s = (b & 0x0FFFFFFFu) * kBlockSamples + jj;
-          out = kw.samples + 3 * (static_cast<size_t>(item - k * kp.P) * kp.ks);
+          out = kw.samples + WPS * (static_cast<size_t>(item - k * kp.P) * kp.ks);
 #ifdef FR_DIAG
           diag_tb = item >> 6;
           diag_seg0 = nseg;
@@ -951,7 +962,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       DIAG_WAVE(DG_END_W);
       DIAG_LANE(DG_END_L);
       V3 col = term;
-      if (DEFER) {
+      if (NIB) {
+        col = V3{__uint_as_float(tsky), __uint_as_float(wnib), 0.0f};
+        wnib = ~0u;  // the next sample starts empty
+      } else if (DEFER) {
         const uint2 w = *drow;
         *drow = make_uint2(~0u, ~0u);  // the next sample starts empty
         col = V3{__uint_as_float(tsky), __uint_as_float(w.x), __uint_as_float(w.y)};
@@ -991,32 +1005,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         }
       }
       if (!staged) {
-        out[3 * jj] = col.x;
-        out[3 * jj + 1] = col.y;
-        out[3 * jj + 2] = col.z;
+        out[WPS * jj] = col.x;
+        out[WPS * jj + 1] = col.y;
+        if (WPS == 3) out[WPS * jj + 2] = col.z;
       } else {
         // stage the colour; every STG-th sample of the block, and its last, go out together
-        float* sl = stage + 3u * (jj & (STG - 1u));
+        float* sl = stage + WPS * (jj & (STG - 1u));
         sl[0] = col.x;
         sl[1] = col.y;
-        sl[2] = col.z;
+        if (WPS == 3) sl[2] = col.z;
         const bool full = (jj & (STG - 1u)) == STG - 1u;
         if (full || s + 1u == s_end) {
-          float* dst = out + 3u * (jj & ~(STG - 1u));
+          float* dst = out + WPS * (jj & ~(STG - 1u));
           if (full && kp.ks == kBlockSamples) {
-            if constexpr ((3u * STG) % 4u == 0u) {
-              // 16-B aligned: item * 192 B + a multiple of 48 B
+            if constexpr ((WPS * STG) % 4u == 0u) {
+              // 16-B aligned: item * 192 (128) B + a multiple of 48 (32) B
               const float4* src = reinterpret_cast<const float4*>(stage);
 #pragma unroll
-              for (uint32_t k = 0; k < 3u * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
+              for (uint32_t k = 0; k < WPS * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
             } else {
               // 8-B aligned: item * 192 B + a multiple of 24 B
               const float2* src = reinterpret_cast<const float2*>(stage);
 #pragma unroll
-              for (uint32_t k = 0; k < 3u * STG / 2u; ++k) reinterpret_cast<float2*>(dst)[k] = src[k];
+              for (uint32_t k = 0; k < WPS * STG / 2u; ++k) reinterpret_cast<float2*>(dst)[k] = src[k];
             }
           } else {
-            for (uint32_t k = 0; k < 3u * ((jj & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
+            for (uint32_t k = 0; k < WPS * ((jj & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
           }
         }
       }
@@ -1069,13 +1083,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 // thread's reads of its own slot bank-conflict free, then summed in sample order. With
 // KF_DEFER the slots hold deferred-unwind records (kDeferUnit) and the colour is rebuilt
 // here from a 12-B-per-entry attenuation table (tile + table fit three workgroups per CU).
+// WPS = 2: 8-B records {t, 4-bit winners} (KF_NIBBLE).
 constexpr uint32_t kSumThreads = 256;
-constexpr uint32_t kSumSlot = 3 * kBlockSamples + 1;  // floats per slot in LDS (odd stride)
 
+template <uint32_t WPS>
 __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const float* __restrict__ samples,
                                                           float* __restrict__ running, float* __restrict__ out_mean,
                                                           uint8_t* __restrict__ out_u8, int first, int last,
                                                           const float4* __restrict__ att, uint32_t n_prims) {
+  constexpr uint32_t kSumSlot = WPS * kBlockSamples + 1;  // floats per slot in LDS (odd stride)
   __shared__ float tile[kSumThreads * kSumSlot];
   __shared__ float att_s[3 * (kDeferUnit + 1)];  // KF_DEFER: attenuation rgb, entry kDeferUnit = 1
   const uint32_t t = threadIdx.x;
@@ -1094,14 +1110,14 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   const bool mt_zero = mt && !(kp.band_h && y / kp.band_h < 4u);  // rows render_mt never fills stay 0
   V3 sum = (first || !valid) ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
   const float fspp = static_cast<float>(kp.spp);
-  const uint32_t per = 3u * kp.ks;  // floats per slot in the buffer
+  const uint32_t per = WPS * kp.ks;  // floats per slot in the buffer
   for (uint32_t bl = 0; bl < kp.nb; ++bl) {
-    const float* src = samples + 3 * (static_cast<size_t>(bl * kp.P + q0) * kp.ks);
+    const float* src = samples + WPS * (static_cast<size_t>(bl * kp.P + q0) * kp.ks);
     __syncthreads();  // the previous block's reads are done (and the table is written)
     if (kp.ks == kBlockSamples) {
-      // all twelve 16-B loads in flight before the LDS writes
-      const float4* src4 = reinterpret_cast<const float4*>(src);  // 192-B slots: 16-B aligned
-      constexpr uint32_t kV = 3u * kBlockSamples / 4u;             // float4 per slot
+      // all twelve (eight) 16-B loads in flight before the LDS writes
+      const float4* src4 = reinterpret_cast<const float4*>(src);  // 192-B (128-B) slots: 16-B aligned
+      constexpr uint32_t kV = WPS * kBlockSamples / 4u;            // float4 per slot
       const uint32_t n4 = nq * kV;
       float4 v[kV];
 #pragma unroll
@@ -1128,8 +1144,18 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
     if (valid && !mt_zero) {
       const uint32_t n = min(kBlockSamples, kp.spp - (kp.b0 + bl) * kBlockSamples);
       const float* c = tile + t * kSumSlot;
-      for (uint32_t j = 0; j < n; ++j, c += 3) {
-        if (defer) {
+      for (uint32_t j = 0; j < n; ++j, c += WPS) {
+        if (WPS == 2) {
+          // 8-B record: terminal, then a_7 ... a_0 from 4-bit entries (kNibbleUnit: 1)
+          const uint32_t tb = __float_as_uint(c[0]), w = __float_as_uint(c[1]);
+          V3 col = tb == kDeferAbsorbed ? V3{0.0f, 0.0f, 0.0f} : sky_from_t(c[0]);
+#pragma unroll
+          for (int k = 7; k >= 0; --k) {
+            const float* e = att_s + 3u * ((w >> (4 * k)) & 0xFu);
+            col = mul(V3{e[0], e[1], e[2]}, col);
+          }
+          sum = add(sum, col);
+        } else if (defer) {
           // the deferred unwind (kDeferUnit): terminal, then a_7 ... a_0 innermost first
           const uint32_t tb = __float_as_uint(c[0]), lo = __float_as_uint(c[1]), hi = __float_as_uint(c[2]);
           V3 col = tb == kDeferAbsorbed ? V3{0.0f, 0.0f, 0.0f} : sky_from_t(c[0]);
@@ -1493,15 +1519,19 @@ static void launch_depth(bool small_depth, const Grid& g, size_t lds, hipStream_
                          const KCam& kc, const KParams& kp, const KWork& kw) {
   if constexpr (!BV && !MT) {
     if (kp.flags & KF_DEFER) {
-      launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, false, false, true>, g, lds, st,
-                        KArgs{ks, kc, kp, kw});
+      if (kp.flags & KF_NIBBLE)
+        launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, false, false, 2>, g, lds, st,
+                          KArgs{ks, kc, kp, kw});
+      else
+        launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, false, false, 1>, g, lds, st,
+                          KArgs{ks, kc, kp, kw});
       return;
     }
   }
   if (small_depth)
-    launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV, MT, false>, g, lds, st, KArgs{ks, kc, kp, kw});
+    launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, BV, MT, 0>, g, lds, st, KArgs{ks, kc, kp, kw});
   else
-    launch_persistent(trace_kernel<KS, HP, FR_KREJ, 0, BV, MT, false>, g, lds, st, KArgs{ks, kc, kp, kw});
+    launch_persistent(trace_kernel<KS, HP, FR_KREJ, 0, BV, MT, 0>, g, lds, st, KArgs{ks, kc, kp, kw});
 }
 
 // BVH kernels walk the list's segments (bvh.h); scenes with planes use the general
@@ -1710,7 +1740,17 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   // §4.5a), so one pass is the default.
   // sample slots per item: a frame of spp < 16 (update()'s 1-spp frames) needs only spp
   kp.ks = p->spp < kBlockSamples ? (p->spp ? p->spp : 1u) : kBlockSamples;
-  const size_t per_block = static_cast<size_t>(kp.P) * kp.ks * 3 * sizeof(float);
+  const bool small_depth = p->max_depth <= kSmallDepth && dc->n < 65536u;
+  // the deferred unwind (kDeferMaxPrims); FR_DEFER=0 keeps the unwind in the trace kernel,
+  // FR_DEFER=1 the 12-B records for small scenes too (A/B)
+  const char* defer_env = getenv("FR_DEFER");
+  const bool defer = small_depth && dc->n <= kDeferMaxPrims && !use_bvh && !(p->flags & FR_FLAG_MT_BANDS) &&
+                     !(defer_env && strcmp(defer_env, "0") == 0);
+  const bool nibble = defer && dc->n <= kNibbleMaxPrims && !(defer_env && strcmp(defer_env, "1") == 0);
+  if (defer) kp.flags |= KF_DEFER;
+  if (nibble) kp.flags |= KF_NIBBLE;
+  const uint32_t wps = nibble ? 2u : 3u;  // words per sample in the buffer
+  const size_t per_block = static_cast<size_t>(kp.P) * kp.ks * wps * sizeof(float);
   // FR_TAIL_PRIO=d: priority from the last 1/d, 1/(4d), 1/(16d) of the queue (0: off)
   uint32_t tail_prio = 8;
   if (const char* e = getenv("FR_TAIL_PRIO")) tail_prio = static_cast<uint32_t>(atoi(e) > 0 ? atoi(e) : 0);
@@ -1766,19 +1806,14 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
     c->ev_trace.push_back(e);
   }
   const size_t n_att = dc->n <= kAttLds ? dc->n : 0u;
-  const bool small_depth = p->max_depth <= kSmallDepth && dc->n < 65536u;
-  // the deferred unwind (kDeferMaxPrims); FR_DEFER=0 keeps the unwind in the trace kernel (A/B)
-  const char* defer_env = getenv("FR_DEFER");
-  const bool defer = small_depth && dc->n <= kDeferMaxPrims && !use_bvh && !(p->flags & FR_FLAG_MT_BANDS) &&
-                     !(defer_env && strcmp(defer_env, "0") == 0);
-  if (defer) kp.flags |= KF_DEFER;
-  const size_t stack_bytes = defer ? kSmallDepth * kBlock * sizeof(uint8_t)
+  const size_t stack_bytes = nibble ? 0u
+                           : defer ? kSmallDepth * kBlock * sizeof(uint8_t)
                            : small_depth ? kSmallDepth * kBlock * sizeof(uint16_t)
                                          : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
                                                sizeof(uint32_t);
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
   const size_t stage_n = stage_samples(use_bvh);
-  const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * 3 * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
+  const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * wps * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
                      n_rec * 64 + stack_bytes + (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
   KWork kw;
   kw.counters = c->d_cnt;
@@ -1841,7 +1876,8 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
     }
     const int first = pass == 0, last = pass + 1 >= passes;
     if (first && c->copy_pending) HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_copy, 0));  // last gather done
-    hipLaunchKernelGGL(sum_kernel, dim3(sum_blocks ? sum_blocks : 1u), dim3(kSumThreads), 0, c->stream_sum, kp, samples,
+    hipLaunchKernelGGL(nibble ? sum_kernel<2> : sum_kernel<3>, dim3(sum_blocks ? sum_blocks : 1u), dim3(kSumThreads), 0,
+                       c->stream_sum, kp, samples,
                        c->d_running, c->d_mean, c->d_u8, first, last, ks.att, dc->n);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev_sum[pass], c->stream_sum));

@@ -558,6 +558,29 @@ def test_bvh_generator_10k_spheres_small(gpu, depth):
     assert st["hits"] > 0
 
 
+@pytest.mark.parametrize("scene,spp", [("scene_08", 3), ("scene_08", 37), ("random", 5)])
+def test_record_formats_are_bit_identical(gpu, scene, spp, monkeypatch):
+    """The deferred unwind stores 8-B records (4-bit winners) for scenes of <= 15
+    primitives and 12-B records (u8 winners) above; FR_DEFER=1 forces the 12-B form and
+    FR_DEFER=0 the unwind in the trace kernel. All three give the same bits."""
+    w, h = 48, 32
+    if scene == "random":
+        prims = [p for p in random_scene(5) if p["kind"] != S.PLANE]
+        sc = gpu.Scene.from_prims(prims)
+        cam = gpu.camera_new(w, h)
+    else:
+        sc = gpu.Scene.from_file(gpu.scene_path(scene), w, h)
+        cam = sc.camera
+    assert len(sc) <= 15
+    monkeypatch.delenv("FR_DEFER", raising=False)
+    ref = gpu.render(sc, cam, w, h, spp, 8)
+    for mode in ("1", "0"):
+        monkeypatch.setenv("FR_DEFER", mode)
+        mean, u8, st = gpu.render(sc, cam, w, h, spp, 8)
+        assert np.array_equal(mean.view(np.uint32), ref[0].view(np.uint32)) and np.array_equal(u8, ref[1]), mode
+        assert (st["segments"], st["hits"], st["scatters"]) == (ref[2]["segments"], ref[2]["hits"], ref[2]["scatters"])
+
+
 @pytest.mark.parametrize("spp", [3, 21])
 def test_bvh_sample_staging_is_bit_identical(gpu, spp, monkeypatch):
     """BVH kernels stage 2 samples per store when the LDS allows (KF_STAGE, the C5 scene);

@@ -11,6 +11,12 @@ if len(sys.argv) > 1:
     a = sys.argv[1:]
     cases = [(a[i], int(a[i + 1]), int(a[i + 2]), int(a[i + 3])) for i in range(0, len(a), 4)]
 for scene, w, h, spp in cases:
-    sc = fr.Scene.from_file(fr.scene_path(scene), w, h)
+    if scene.startswith("gen:"):  # gen:COUNT:MESH, the generator scene (tools/gen_scene.py)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import gen_scene
+        _, count, mesh = scene.split(":")
+        sc = fr.Scene.from_json(gen_scene.dumps(gen_scene.generator_scene(int(count), mesh)), w, h)
+    else:
+        sc = fr.Scene.from_file(fr.scene_path(scene), w, h)
     m, u, st = fr.render(sc, sc.camera, w, h, spp, 8)
     print(scene, w, h, spp, st, flush=True)

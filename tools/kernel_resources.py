@@ -15,7 +15,7 @@ for line in open(sys.argv[1]):
         if m and cur is not None:
             cur[key.split()[0]] = int(m.group(1))
 for r in rows:
-    m = re.search(r"trace_kernelILi(\d)ELb(\d)ELi\d+ELi(\d)ELb(\d)ELb(\d)ELb(\d)E", r["name"])
+    m = re.search(r"trace_kernelILi(\d)ELb(\d)ELi\d+ELi(\d)ELb(\d)ELb(\d)ELi(\d)E", r["name"])
     if m:
         print("KS=%s HP=%s MAXD=%s BVH=%s MT=%s DEFER=%s" % m.groups(), "VGPR", r.get("VGPRs"), "SGPR",
               r.get("TotalSGPRs"), "occ", r.get("Occupancy"), "spill", r.get("SGPRs"))
