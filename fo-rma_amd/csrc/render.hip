@@ -392,7 +392,10 @@ template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, int DEF
 #ifdef FR_MIN_WAVES
 #define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(FR_MIN_WAVES)))
 #else
-#define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(BVH ? 6 : 7)))
+#ifndef FR_NIB_WAVES
+#define FR_NIB_WAVES 7
+#endif
+#define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(BVH ? 6 : DEFER == 2 ? FR_NIB_WAVES : 7)))
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) FR_OCC_ATTR void trace_kernel(
     KArgs args) {
@@ -928,30 +931,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
             n = obb_normal(xyz(b1), xyz(b2), xyz(b3), sl, closest, f.dl);
           }
           const V3 p = HAS_PLANE ? add(o, scl(t_last, d)) : pw;
+          // Written for every hit lane, so that only the rarer materials' values are set
+          // under a branch (fewer register copies where the branches join): an absorbed
+          // path (SC_NONE) ends here and its o, d and sbest are not read again.
+          const V3 din = d;
+          o = p;
+          d = add(p, n);  // lambertian / light: target = (p + n) + rus
+          sbest = static_cast<uint32_t>(best);
+          smetal = c == SC_METAL;
+          ended = c == SC_NONE;
+          if (c != SC_NONE && c != SC_DIELECTRIC) need = NEED_SPHERE;
           if (c == SC_DIELECTRIC) {
             // one draw, no rejection loop (sphere.rs:107-145)
-            const V3 nd = scatter_dielectric(d, n, rng);
+            d = scatter_dielectric(din, n, rng);
             push(static_cast<uint32_t>(best));
             ++depth;
             ++nscat;
-            o = p;
-            d = nd;
             have_ray = true;
-            ended = false;
-          } else if (c != SC_NONE) {
-            // lambertian / light: target = (p + n) + rus; metal: reflect(unit(d), n) + fuzz * rus
-            sbest = static_cast<uint32_t>(best);
-            smetal = c == SC_METAL;
-            if (smetal) {
-              sfuzz = sc.mat[best].w;
-              sn = n;
-              d = reflect(unit(d), n);
-            } else {
-              d = add(p, n);
-            }
-            o = p;
-            need = NEED_SPHERE;
-            ended = false;
+          } else if (smetal) {
+            // metal: reflect(unit(d), n) + fuzz * rus
+            sfuzz = sc.mat[best].w;
+            sn = n;
+            d = reflect(unit(din), n);
           }
         }
       }
