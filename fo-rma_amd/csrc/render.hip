@@ -160,7 +160,6 @@ struct KParams {
   float rW, rH;                       // RN(1 / W), RN(1 / H) (host IEEE division)
   uint32_t row_magic, row_shift;      // x / tiles_per_row = fastdiv(x, row_magic, row_shift)
   uint32_t band_h;                    // FR_FLAG_MT_BANDS: rows per band, H / 4 (tracer.rs:87)
-  uint32_t prio_at[3];  // a wave reserving a batch at or past prio_at[k] raises its priority to k + 1
   uint32_t ks;          // sample slots per work item in the sample buffer: min(spp, kBlockSamples)
   // items handed out without the queue: wave w of the grid starts on batch w (one batch
   // per wave, n_static = waves x 64); the queue counts from n_static
@@ -594,13 +593,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           st = st2;
           xy = xy2;
           b = b2;
-        }
-        // Queue tail: the waves that claim last hold the longest remaining work, so they
-        // get issue priority over waves finishing older items (shortens the drain).
-        if (base >= kg.prio_at[0]) {
-          if (base >= kg.prio_at[2]) __builtin_amdgcn_s_setprio(3);
-          else if (base >= kg.prio_at[1]) __builtin_amdgcn_s_setprio(2);
-          else __builtin_amdgcn_s_setprio(1);
         }
       }
       q_next = grab ? base + (n - avail) : next + n;
@@ -1752,9 +1744,6 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   if (nibble) kp.flags |= KF_NIBBLE;
   const uint32_t wps = nibble ? 2u : 3u;  // words per sample in the buffer
   const size_t per_block = static_cast<size_t>(kp.P) * kp.ks * wps * sizeof(float);
-  // FR_TAIL_PRIO=d: priority from the last 1/d, 1/(4d), 1/(16d) of the queue (0: off)
-  uint32_t tail_prio = 8;
-  if (const char* e = getenv("FR_TAIL_PRIO")) tail_prio = static_cast<uint32_t>(atoi(e) > 0 ? atoi(e) : 0);
   uint32_t want_passes = 1;
   if (const char* e = getenv("FR_PIPELINE")) want_passes = static_cast<uint32_t>(atoi(e) > 0 ? atoi(e) : 1);
   uint32_t passes_u = nblocks ? (want_passes < nblocks ? want_passes : nblocks) : 0u;
@@ -1853,8 +1842,6 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
       kp.b_fine = nblocks - 1u;
       kp.n_items = kp.n_coarse + ((n_last + kFineSamples - 1u) / kFineSamples) * kp.P;
     }
-    for (int k = 0; k < 3; ++k)
-      kp.prio_at[k] = tail_prio ? kp.n_items - kp.n_items / (tail_prio << (2 * k)) : 0xFFFFFFFFu;
     if (kp.n_items) {
       if (pass >= 2) HIPCHK(hipStreamWaitEvent(ts, c->ev_sum[pass - 2], 0));  // the slot's last reader is done
       kw.queue = reinterpret_cast<uint32_t*>(c->d_cnt + 31 - slot);
