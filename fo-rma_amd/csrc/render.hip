@@ -192,8 +192,9 @@ static void fastdiv_magic(uint32_t d, uint32_t& m, uint32_t& shifts) {
 // Work buffers of one render pass.
 struct KWork {
   uint32_t* queue;            // next unclaimed item (zeroed before the pass)
-  // per-sample colours, item-major: sample s of item (b, q) at [(item * ks + s - 16 b)] x 3 f32,
-  // item = (b - b0) * P + q, so one item's samples are contiguous (192 B at ks = 16)
+  // per-sample colours or deferred records, item-major: sample s of item (b, q) at
+  // [(item * ks + s - 16 b)] x WPS words (3, or 2 for 8-B records), item = (b - b0) * P + q,
+  // so one item's samples are contiguous (192 or 128 B at ks = 16)
   float* samples;
   unsigned long long* counters;  // [0] segments, [1] hits, [2] scatters (reduce_counters)
   // per-wave partial counters, [wave][3], stored by every wave of the grid and summed
@@ -259,9 +260,9 @@ __device__ __forceinline__ uint32_t buf_load1(const void* base, uint32_t byte_of
 constexpr uint32_t kAttLds = 1024;  // attenuation/class entries staged in LDS (16 B each)
 constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for small scenes
 // Sample colours a lane stages in LDS before storing them to the (item-major) sample
-// buffer: 4 x 12 B = three 16-B stores per 4 samples instead of four scattered 12-B
-// stores, which L2 wrote back as partial lines (3.5x WRITE_SIZE). The BVH kernels keep
-// their LDS for the traversal stack (occupancy) and store each sample directly.
+// buffer: 4 x 12 B = three 16-B stores per 4 samples (4 x 8 B = two, for 8-B records)
+// instead of four scattered stores, which L2 wrote back as partial lines (3.5x WRITE_SIZE).
+// The BVH kernels stage 2 samples when their LDS allows (below).
 #ifndef FR_STAGE
 #define FR_STAGE 4  // 1 or 4 (A/B builds)
 #endif
@@ -1071,7 +1072,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 // Adds each pixel's sample colours of this pass, in sample order, onto its running
 // sum (tracer.rs:174); the last pass divides by spp, gamma-corrects and quantises
 // (tracer.rs:177-184). One thread per pixel slot. A workgroup's 256 slots of one sample
-// block are one contiguous run of the item-major buffer (256 x 192 B at ks = 16): it is
+// block are one contiguous run of the item-major buffer (256 x 192 B, or 128 B for 8-B
+// records, at ks = 16): it is
 // read with coalesced 16-B loads into an LDS tile whose odd slot stride keeps each
 // thread's reads of its own slot bank-conflict free, then summed in sample order. With
 // KF_DEFER the slots hold deferred-unwind records (kDeferUnit) and the colour is rebuilt
