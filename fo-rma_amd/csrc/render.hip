@@ -788,8 +788,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               DIAG_WAVE(DG_NODE_W);
               DIAG_LANE(DG_NODE_L);
               // internal node: both children's boxes
-              const float4 na = sc.bvh[4 * ref], nb = sc.bvh[4 * ref + 1], nc = sc.bvh[4 * ref + 2];
-              const uint4 nr = reinterpret_cast<const uint4*>(sc.bvh)[4 * ref + 3];
+              float4 na, nb, nc;
+              uint4 nr;
+              const uint32_t ref0 = __builtin_amdgcn_readfirstlane(ref);
+              if (__ballot(ref != ref0) == 0) {
+                // every walking lane is at the same node (coherent rays near the root):
+                // scalar loads, which return sooner than the vector path
+                const RecRef nd = rec_at(sc.bvh, ref0);
+                na = nd[0];
+                nb = nd[1];
+                nc = nd[2];
+                const float4 r = nd[3];
+                nr = make_uint4(__float_as_uint(r.x), __float_as_uint(r.y), __float_as_uint(r.z), __float_as_uint(r.w));
+              } else {
+                na = sc.bvh[4 * ref];
+                nb = sc.bvh[4 * ref + 1];
+                nc = sc.bvh[4 * ref + 2];
+                nr = reinterpret_cast<const uint4*>(sc.bvh)[4 * ref + 3];
+              }
               const Slab sl = slab3_fused(xyz(na), xyz(nb), oinv, invc);
               const Slab sr = slab3_fused(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, oinv, invc);
               const bool hl = (sl.tn <= sl.tf) & (sl.tf >= 0.001f) & (sl.tn <= closest);
