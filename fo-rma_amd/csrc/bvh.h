@@ -39,7 +39,7 @@ struct BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode is four float4");
 
-constexpr uint32_t kBvhLeafMax = 4;    // primitives per leaf (more only for huge scenes)
+constexpr uint32_t kBvhLeafMax = 4;    // primitives per leaf of sphere-only lists (2 for others; more only for huge scenes)
 // The in-order loop (wave-uniform, scalar loads) beats the per-lane walk only for small
 // lists: weight box / sphere 1, oriented box 2, triangle 2.5. Measured at 1080p
 // (tools/bvh_threshold.sh): 43 mixed prims (scene_01) 38 ms in order vs 55 BVH; 50
