@@ -1122,20 +1122,26 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   V3 sum = (first || !valid) ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
   const float fspp = static_cast<float>(kp.spp);
   const uint32_t per = WPS * kp.ks;  // floats per slot in the buffer
+  // full 16-sample slots: block bl + 1's loads are issued before block bl is summed, so
+  // they are in flight during the sum (a shard at N = 8 gives each workgroup's thread a
+  // chain of 16 dependent block loads)
+  constexpr uint32_t kV = WPS * kBlockSamples / 4u;  // float4 per slot
+  const uint32_t n4 = nq * kV;
+  float4 v[kV];
+  auto load_block = [&](uint32_t bl) {
+    // 192-B (128-B) slots: 16-B aligned
+    const float4* src4 = reinterpret_cast<const float4*>(samples + WPS * (static_cast<size_t>(bl * kp.P + q0) * kp.ks));
+#pragma unroll
+    for (uint32_t k = 0; k < kV; ++k) {
+      const uint32_t i = t + k * kSumThreads;
+      if (i < n4) v[k] = src4[i];
+    }
+  };
+  if (kp.ks == kBlockSamples && kp.nb) load_block(0);
   for (uint32_t bl = 0; bl < kp.nb; ++bl) {
     const float* src = samples + WPS * (static_cast<size_t>(bl * kp.P + q0) * kp.ks);
     __syncthreads();  // the previous block's reads are done (and the table is written)
     if (kp.ks == kBlockSamples) {
-      // all twelve (eight) 16-B loads in flight before the LDS writes
-      const float4* src4 = reinterpret_cast<const float4*>(src);  // 192-B (128-B) slots: 16-B aligned
-      constexpr uint32_t kV = WPS * kBlockSamples / 4u;            // float4 per slot
-      const uint32_t n4 = nq * kV;
-      float4 v[kV];
-#pragma unroll
-      for (uint32_t k = 0; k < kV; ++k) {
-        const uint32_t i = t + k * kSumThreads;
-        if (i < n4) v[k] = src4[i];
-      }
 #pragma unroll
       for (uint32_t k = 0; k < kV; ++k) {
         const uint32_t i = t + k * kSumThreads;
@@ -1148,6 +1154,7 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
           d[3] = v[k].w;
         }
       }
+      if (bl + 1u < kp.nb) load_block(bl + 1u);
     } else {
       for (uint32_t i = t; i < nq * per; i += kSumThreads) tile[(i / per) * kSumSlot + i % per] = src[i];
     }
