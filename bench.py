@@ -21,7 +21,9 @@ Rank 0 prints one JSON line with:
   157.3 TFLOP/s peak, plus the VALU issue fraction and HBM traffic read from rocprofv3
   hardware counters in this run (a child process, N=1 only);
 - hbm_roofline: algorithmic bytes per launch against 8 TB/s (the north star's ask);
-- cpu_baseline (N=1): the oracle on this host's cores, all of them and one.
+- cpu_baseline (N=1): the oracle on this host's cores, all of them and one; its `c1`
+  entry is BASELINE config C1 (scene_01 256x256/4 spp/4 bounces, the reference's CPU
+  case) in full on the oracle (1 thread, all threads) and on the GPU, compared bit for bit.
 """
 import argparse
 import glob
@@ -255,6 +257,47 @@ def cpu_baseline(budget_s=12.0):
     return omp
 
 
+def config_c1(ctx, steps=5):
+    """BASELINE config C1 (scene_01 at 256x256, 4 spp, 4 bounces; the reference's CPU
+    plumbing case, tracer.rs:160-187) in full: the oracle as `cpu-ref` (1 thread) and
+    `cpu-omp` (every core of the affinity mask), and the HIP path on this rank's device
+    (render + gather per step, after one warm-up), with the frames compared bit for bit."""
+    import numpy as np
+
+    from oracle import oracle_py, scene_ref
+    import forma_rt as fr
+
+    w, h, spp, depth, name = 256, 256, 4, 4, "scene_01"
+    prims, (frm, at, vup, fov) = scene_ref.load_json(open(fr.scene_path(name)).read())
+    cam = oracle_py.camera_look(frm, at, vup, fov, 0.1, w, h)
+    threads = max(1, host_info()["affinity"])
+    out = {"config": f"{name} {w}x{h} {spp}spp {depth} bounces (BASELINE config 1), full frame", "samples": w * h * spp}
+    ref = None
+    for label, nt in (("cpu_ref", 1), ("cpu_omp", threads)):
+        t = time.perf_counter()
+        omean, ou8, cnt, _ = oracle_py.render(prims, cam, w, h, spp, depth, SEED, threads=nt)
+        dt = time.perf_counter() - t
+        ref = ref or (omean, ou8)
+        out[label] = {"value": round(cnt["samples"] / dt / 1e6, 4), "unit": "Msamples/s", "cores": nt,
+                      "kind": "port", "ms": round(dt * 1e3, 3)}
+    sc = fr.Scene.from_file(fr.scene_path(name), w, h)
+    params = fr.make_params(w, h, spp, depth, SEED)
+    frame = fr.PinnedFrame(w, h)
+    run_steps(ctx, sc, sc.camera, params, frame, 1)
+    device_sync(ctx)
+    t = time.perf_counter()
+    run_steps(ctx, sc, sc.camera, params, frame, steps)
+    device_sync(ctx)
+    dt = (time.perf_counter() - t) / steps
+    out["gpu"] = {"value": round(w * h * spp / dt / 1e6, 3), "unit": "Msamples/s", "ms_per_step": round(dt * 1e3, 4),
+                  "step": "render + D2H gather"}
+    mean, u8 = frame.mean.reshape(h, w, 3), frame.u8.reshape(h, w, 3)
+    out["gpu"]["max_abs_diff_vs_cpu_ref"] = float(np.max(np.abs(mean - ref[0])))
+    out["gpu"]["u8_identical"] = bool(np.array_equal(u8, ref[1]))
+    frame.close()
+    return out
+
+
 # ---- the run --------------------------------------------------------------------
 
 class Barrier:
@@ -425,6 +468,10 @@ def main():
     if world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_budget)
         out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
+        try:
+            out["cpu_baseline"]["c1"] = config_c1(ctx)
+        except Exception as e:  # reported in the line; the headline above stands on its own
+            out["cpu_baseline"]["c1"] = {"error": f"{type(e).__name__}: {e}"}
     print(json.dumps(out), flush=True)
     frame.close()
     ctx.close()
