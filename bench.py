@@ -9,7 +9,9 @@ One process per GPU. A step renders the whole frame and gathers it to the host: 
 renders the 8-row strips k with k % N == r (no collective on the data path) and copies
 its strips (f32 means and the u8 image) into page-locked host memory, the "final gather
 to host" (BASELINE.md §4). The gather of frame k runs on its own stream while frame k+1
-traces; the timed region ends only when the last frame's gather has landed. The timed
+traces; the frames are enqueued back to back with no host wait between them (run_steps;
+--sync-each waits for every frame's stats); the timed region ends only when the last
+frame's gather has landed. The timed
 region is K steps bracketed by a barrier and a device synchronize on both sides; the
 time is the max over ranks; value = all samples of the K frames / that time. Inputs
 (scene, camera) are resident on the device before timing.
@@ -336,15 +338,28 @@ def device_sync(ctx):
         torch.cuda.synchronize()
 
 
-def run_steps(ctx, scene, cam, params, frame, steps):
+def run_steps(ctx, scene, cam, params, frame, steps, sync_each=False):
     """Render `steps` frames of this rank's shard, each followed by its asynchronous gather
-    into the pinned host frame; returns per-step stats."""
-    stats = []
+    into the pinned host frame; returns per-step stats.
+
+    By default the frames are enqueued back to back with no host wait between them, as a
+    renderer streaming frames runs: the context's streams order frame k+1's trace after
+    frame k's sum, its sum after frame k's gather (fr_ctx_download_async), so every frame
+    is rendered and gathered in full, and the GPU does not idle while the host reads a
+    frame's counters and enqueues the next. The counters and event times are then the last
+    frame's, which are every frame's (the same deterministic work). sync_each=True waits
+    for each frame's stats before enqueueing the next (round-2 behaviour, --sync-each)."""
+    if sync_each:
+        stats = []
+        for _ in range(steps):
+            ctx.render(scene, cam, params)
+            stats.append(ctx.sync())
+            ctx.download_async(frame)
+        return stats
     for _ in range(steps):
         ctx.render(scene, cam, params)
-        stats.append(ctx.sync())
         ctx.download_async(frame)
-    return stats
+    return [ctx.sync()] * steps if steps else []
 
 
 def main():
@@ -356,6 +371,7 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--verify", action="store_true", help="stitch the frame on rank 0 and report a checksum")
+    ap.add_argument("--sync-each", action="store_true", help="wait for each frame's stats before the next")
     a = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -384,12 +400,12 @@ def main():
     ctx = fr.RenderContext(local)
     frame = fr.PinnedFrame(WIDTH, HEIGHT)
 
-    run_steps(ctx, scene, cam, params, frame, a.warmup)
+    run_steps(ctx, scene, cam, params, frame, a.warmup, a.sync_each)
     device_sync(ctx)
     barrier()
     device_sync(ctx)
     t0 = time.perf_counter()
-    stats = run_steps(ctx, scene, cam, params, frame, a.steps)
+    stats = run_steps(ctx, scene, cam, params, frame, a.steps, a.sync_each)
     device_sync(ctx)  # the last frame's gather has landed
     t1 = time.perf_counter()
     barrier()
@@ -444,6 +460,7 @@ def main():
                    "scene": SCENE, "width": WIDTH, "height": HEIGHT, "spp": SPP, "max_depth": DEPTH, "seed": SEED,
                    "parallelism": f"row-strips x{world}"},
         "step": "render of the rank's strips + D2H gather of its f32 means and u8 image into pinned host memory",
+        "host_sync": "each step" if a.sync_each else "after the K steps (frames streamed back to back)",
         "render_only_value": round(render_only, 3),
         "render_only_ms_per_step": round(kernel_ms_max, 3),
         "segments_per_sample": round(total_segs / max(1.0, total_samples), 4),
