@@ -348,6 +348,32 @@ def test_context_reuse_and_scene_edits(gpu):
     ctx.close()
 
 
+@pytest.mark.parametrize("shard", [(0, 1), (1, 3)])
+def test_streamed_frames_match_the_oracle(gpu, shard):
+    """bench.py's loop: frames enqueued back to back on one context, each followed by its
+    asynchronous gather into the same pinned host frame, one sync after the last. The
+    streams alone order the frames, so the host frame holds the last frame's strips
+    exactly, and the counters are that frame's."""
+    w, h, spp, depth = 64, 40, 20, 8
+    sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
+    prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path("scene_08")).read())
+    cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
+    omean, ou8, ocnt, _ = O.render(prims, cam, w, h, spp, depth, threads=8, shard_index=shard[0],
+                                   shard_count=shard[1])
+    rows = [y for y in range(h) if (y // 8) % shard[1] == shard[0]]
+    p = gpu.make_params(w, h, spp, depth, shard_index=shard[0], shard_count=shard[1])
+    ctx = gpu.RenderContext(0)
+    frame = gpu.PinnedFrame(w, h)
+    for _ in range(4):
+        ctx.render(sc, sc.camera, p)
+        ctx.download_async(frame)
+    st = ctx.sync()
+    ctx.wait()
+    assert_parity(frame.mean.copy(), frame.u8.copy(), st, omean, ou8, ocnt, rows=rows)
+    frame.close()
+    ctx.close()
+
+
 def test_update_and_save_image_mirror(gpu, tmp_path):
     w, h = 40, 30
     m = gpu.create_model(w, h)
