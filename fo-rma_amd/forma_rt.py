@@ -433,6 +433,13 @@ class RenderContext:
                                     u8.ctypes.data_as(C.POINTER(C.c_uint8))))
         return mean, u8
 
+    def download_into(self, mean=None, u8=None):
+        """Copy the last render's strips into caller-owned full-image arrays (either may be
+        None: that output is not copied). Page-locked arrays (PinnedFrame) copy by DMA."""
+        fp = None if mean is None else mean.ctypes.data_as(C.POINTER(C.c_float))
+        up = None if u8 is None else u8.ctypes.data_as(C.POINTER(C.c_uint8))
+        check(lib().fr_ctx_download(self._h, fp, up))
+
     def download_async(self, frame):
         """Enqueue the last render's D2H gather into `frame` (a PinnedFrame); returns at
         once. The copies finish before wait() returns and before the next render writes
@@ -515,6 +522,7 @@ class TraceModel:
         self.device = 0
         self.ctx = None
         self.last_stats = None
+        self._pinned = None  # page-locked home of `pixels` once update() runs on the device
 
     def context(self):
         if self.ctx is None:
@@ -530,7 +538,24 @@ class TraceModel:
         mean, u8 = ctx.download(self.width, self.height)
         return mean, u8, self.last_stats
 
+    def frame_u8(self, scene, max_depth, seed):
+        """update()'s frame: 1 spp, only the u8 image copied back, by DMA into page-locked
+        memory that `pixels` views (overwritten by the next frame, as tracer.rs's
+        model.pixels is)."""
+        ctx = self.context()
+        ctx.render(scene, self.scene.camera, make_params(self.width, self.height, 1, max_depth, seed))
+        self.last_stats = ctx.sync()
+        if self._pinned is None:
+            self._pinned = PinnedFrame(self.width, self.height)
+        ctx.download_into(u8=self._pinned.u8)
+        self.pixels = self._pinned.u8.reshape(-1)
+        return self.pixels
+
     def close(self):
+        if self._pinned is not None:
+            self.pixels = np.array(self.pixels)  # keep the last frame past the pinned buffer
+            self._pinned.close()
+            self._pinned = None
         if self.ctx is not None:
             self.ctx.close()
             self.ctx = None
@@ -553,9 +578,7 @@ def update(model, keys, delta_time, max_depth=MAX_DEPTH):
     camera_orbit(model.scene.camera, list(d))
     seed = model.seed ^ (0x9E3779B97F4A7C15 * (model.frame + 1) & 0xFFFFFFFFFFFFFFFF)
     model.frame += 1
-    _, u8, _ = model.render(model.scene, 1, max_depth, seed)
-    model.pixels = u8.reshape(-1)
-    return model.pixels
+    return model.frame_u8(model.scene, max_depth, seed)
 
 
 def write_png(path, rgb8):
