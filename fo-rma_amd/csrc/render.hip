@@ -67,6 +67,12 @@ constexpr uint32_t kMaxWgPerCu = 8;   // 2048 threads per CU / kBlock: the persi
 #ifndef FR_KREJ
 #define FR_KREJ 4  // rejection loop: lanes left to the next iteration (tuning only, results unchanged)
 #endif
+// ... for the 8-B-record kernels (scenes of <= 15 primitives, the headline's): measured
+// C3 trace 20.81 -> 20.69 ms at 6 (7 and 8 the same within noise); 6 on the other kernels
+// cost C2 +1.7 % and a 10k-sphere BVH frame +1.2 %, so they keep FR_KREJ
+#ifndef FR_KREJ_NIB
+#define FR_KREJ_NIB 6
+#endif
 #ifndef FR_NUM_SGPR
 #define FR_NUM_SGPR 96
 #endif
@@ -1538,7 +1544,7 @@ static void launch_depth(bool small_depth, const Grid& g, size_t lds, hipStream_
   if constexpr (!BV && !MT) {
     if (kp.flags & KF_DEFER) {
       if (kp.flags & KF_NIBBLE)
-        launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, false, false, 2>, g, lds, st,
+        launch_persistent(trace_kernel<KS, HP, FR_KREJ_NIB, kSmallDepth, false, false, 2>, g, lds, st,
                           KArgs{ks, kc, kp, kw});
       else
         launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, false, false, 1>, g, lds, st,
