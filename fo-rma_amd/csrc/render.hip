@@ -399,7 +399,9 @@ template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, int DEF
 #define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(FR_MIN_WAVES)))
 #else
 #ifndef FR_NIB_WAVES
-#define FR_NIB_WAVES 7
+// the 8-B-record (headline) kernel at 8 waves: with FR_KREJ_NIB = 6, C3 trace 20.67 ->
+// 20.49 ms and shard 0/4 -0.6 % (shard 0/8 +0.3 %); at KREJ 4 it had measured -0.3 % / +1.1 %
+#define FR_NIB_WAVES 8
 #endif
 #define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(BVH ? 6 : DEFER == 2 ? FR_NIB_WAVES : 7)))
 #endif
