@@ -30,6 +30,7 @@ Rank 0 prints one JSON line with:
 import argparse
 import glob
 import json
+import math
 import os
 import re
 import shutil
@@ -47,6 +48,11 @@ SCENE = "scene_08"
 WIDTH, HEIGHT, SPP, DEPTH, SEED = 1920, 1080, 256, 8, 0x5EED
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, chip-level parameters (spec)
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, peak FP32 vector (spec)
+# The ceiling parity allows: no FMA contraction, so one f32 op per lane per issue slot:
+# 256 CUs x 4 SIMDs x 32 lanes/clk (a wave64 VALU instruction issues over 2 cycles,
+# MI355X_MICROARCH.md) x 2.4 GHz = 78.6 Tops/s, half the 157.3 TFLOP/s FMA peak. (SURVEY.md
+# §8d's 39.3 assumed 157.3 counted packed FMA, i.e. 16 lanes/clk per SIMD.)
+NO_FMA_PEAK_TOPS = 78.6
 N_SIMDS = 1024             # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues over 2 cycles
 FLOPS_H = os.path.join(ROOT, "fo-rma_amd", "csrc", "flops.h")
 
@@ -215,16 +221,28 @@ def host_info():
     return info
 
 
-def cpu_baseline(budget_s=12.0):
+def cpu_threads(host):
+    """Threads the CPU baseline runs on: the affinity mask capped at the cgroup CPU quota
+    (rounded up), i.e. the cores this process can actually use at once."""
+    n = max(1, host["affinity"])
+    q = host.get("cgroup_cpus")
+    if q:
+        n = min(n, max(1, math.ceil(q)))
+    return n
+
+
+def cpu_baseline(budget_s=12.0, single_s=3.0):
     """The oracle (oracle/oracle.cpp, a C++ restatement of tracer.rs's save_image) on
-    this host, over a bounded row sample of the same workload: `cpu-omp` on every core
-    this process may run on (rows and 32-pixel chunks over threads, the render_mt
-    shape), and `cpu-ref` on one thread (the save_image shape)."""
+    this host, over a bounded row sample of the same workload: `cpu-omp` (rows and
+    32-pixel chunks over threads, the render_mt shape) on as many threads as the process
+    has CPUs (affinity mask capped at the cgroup quota: `cores`), the same sample on every
+    thread of the affinity mask when that is more (`oversubscribed`, reported only), and
+    `cpu-ref` on one thread (the save_image shape) for at least 2 s."""
     from oracle import oracle_py, scene_ref
     import forma_rt as fr
 
     host = host_info()
-    threads = max(1, host["affinity"])
+    threads = cpu_threads(host)
     prims, (frm, at, vup, fov) = scene_ref.load_json(open(fr.scene_path(SCENE)).read())
     cam = oracle_py.camera_look(frm, at, vup, fov, 0.1, WIDTH, HEIGHT)
 
@@ -247,11 +265,24 @@ def cpu_baseline(budget_s=12.0):
     omp = {"value": round(cnt["samples"] / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
            "sample": f"{rows} of {HEIGHT} rows (every {step}th) of {SCENE} {WIDTH}x{HEIGHT} {SPP}spp depth {DEPTH}, "
                      f"{cnt['samples']} samples in {dt:.2f}s on {threads} threads, oracle/oracle.cpp (-O2)",
+           "threads_rule": "min(affinity mask, ceil(cgroup CPU quota))",
            "segments_per_sample": round(cnt["segments"] / max(1, cnt["samples"]), 4), "host": host}
-    # one thread: the same rows, every cstep-th pixel of them, sized to a third of the budget
-    # assuming at most linear scaling (a thread is at least 1/threads of the whole)
-    cstep = max(1, int(threads * 3))
+    if host["affinity"] > threads:
+        cnt2, rows2, dt2 = timed(step, host["affinity"])
+        omp["oversubscribed"] = {"value": round(cnt2["samples"] / dt2 / 1e6, 4), "unit": "Msamples/s",
+                                 "threads": host["affinity"],
+                                 "sample": f"the same {rows2} rows on every thread of the affinity mask "
+                                           f"({host['affinity']} threads in a {host.get('cgroup_cpus')}-CPU quota): "
+                                           f"{cnt2['samples']} samples in {dt2:.2f}s"}
+    # one thread: the same rows, every cstep-th pixel, sized to `single_s` seconds from the
+    # multi-thread rate (a thread does at most that rate / 1 and at least / threads)
+    per_sample_1 = dt / max(1, cnt["samples"]) * threads
+    pix = rows * WIDTH
+    cstep = max(1, int(pix * SPP * per_sample_1 / single_s))
     cnt1, rows1, dt1 = timed(step, 1, col_step=cstep)
+    while dt1 < 2.0 and cstep > 1:  # scaling was sub-linear: a larger sample, until >= 2 s
+        cstep = max(1, int(cstep * dt1 / single_s))
+        cnt1, rows1, dt1 = timed(step, 1, col_step=cstep)
     omp["single_thread"] = {"value": round(cnt1["samples"] / dt1 / 1e6, 4), "unit": "Msamples/s", "cores": 1,
                             "kind": "port", "sample": f"the same {rows1} rows, every {cstep}th pixel: "
                                                       f"{cnt1['samples']} samples in {dt1:.2f}s "
@@ -272,7 +303,7 @@ def config_c1(ctx, steps=5):
     w, h, spp, depth, name = 256, 256, 4, 4, "scene_01"
     prims, (frm, at, vup, fov) = scene_ref.load_json(open(fr.scene_path(name)).read())
     cam = oracle_py.camera_look(frm, at, vup, fov, 0.1, w, h)
-    threads = max(1, host_info()["affinity"])
+    threads = cpu_threads(host_info())
     out = {"config": f"{name} {w}x{h} {spp}spp {depth} bounces (BASELINE config 1), full frame", "samples": w * h * spp}
     ref = None
     for label, nt in (("cpu_ref", 1), ("cpu_omp", threads)):
@@ -402,6 +433,7 @@ def main():
 
     run_steps(ctx, scene, cam, params, frame, a.warmup, a.sync_each)
     device_sync(ctx)
+    ctx.trace_log(True)  # HIP events around every trace launch and render of the K frames
     barrier()
     device_sync(ctx)
     t0 = time.perf_counter()
@@ -410,15 +442,19 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = barrier.max(t1 - t0)
+    launch_log = ctx.trace_log_read()             # every trace launch of the K frames (ms)
+    frame_log = ctx.trace_log_read(frames=True)   # every render of the K frames (ms)
+    ctx.trace_log(False)
 
     n = max(1, len(stats))
     my_samples = sum(s["samples"] for s in stats)
     total_samples = barrier.sum(my_samples)
     counts = {k: sum(s[k] for s in stats) / n for k in ("segments", "hits", "scatters", "samples")}
-    kernel_ms = sum(s["kernel_ms"] for s in stats) / n        # the render on its streams (trace + sum)
-    trace_ms = sum(s["trace_ms"] for s in stats) / n          # trace_kernel launches of one frame
     launches = max(1, stats[0]["trace_launches"])              # sample-block passes
-    launch_ms = trace_ms / launches                            # what rocprof's average reports
+    # means over all K frames from the launch log (not the last frame's events)
+    kernel_ms = sum(frame_log) / max(1, len(frame_log))        # the render on its streams (trace + sum)
+    launch_ms = sum(launch_log) / max(1, len(launch_log))      # what rocprof's average reports
+    trace_ms = launch_ms * launches                            # trace_kernel launches of one frame
     kernel_ms_max = barrier.max(kernel_ms)
     render_only = barrier.sum(my_samples / n) / (kernel_ms_max * 1e-3) / 1e6
     total_segs = barrier.sum(counts["segments"] * n)
@@ -468,9 +504,14 @@ def main():
         "trace_kernel_ms": round(trace_ms, 3),
         "trace_launches": launches,
         "trace_kernel_ms_per_launch": round(launch_ms, 3),
+        "trace_kernel_ms_min_max": [round(min(launch_log), 3), round(max(launch_log), 3)] if launch_log else None,
+        "timing_source": f"HIP events around each of the {len(launch_log)} trace launches and {len(frame_log)} "
+                         "renders of the K timed frames (fr_ctx_trace_log), averaged",
         "occupancy_wg_per_cu": stats[0]["occupancy"],
         "roofline": {"bound": "valu", "achieved": round(tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(tflops / FP32_PEAK_TFLOPS, 5), "traffic": round(traffic) if traffic else None,
+                     "peak_no_fma": NO_FMA_PEAK_TOPS, "frac_no_fma": round(tflops / NO_FMA_PEAK_TOPS, 5),
+                     "peak_no_fma_rule": "1024 SIMDs x 32 lanes/clk x 2.4 GHz (no contraction: 1 op per lane-slot)",
                      "kernel": "trace_kernel", "flops_per_launch": round(flops_launch),
                      "flop_model": "fo-rma_amd/csrc/flops.h x exact counters", "valu_issue": issue},
         "hbm_roofline": {"bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -21,6 +21,8 @@
 #include <string.h>
 #include <chrono>
 #include <cmath>
+#include <algorithm>
+#include <string>
 #include <thread>
 
 #include "bvh.h"
@@ -59,6 +61,25 @@ __device__ unsigned long long g_fr_iter_times[1024 * 1024];
   } while (0)
 
 namespace fr {
+
+// Sets a call's device and restores the caller's current device when the call returns,
+// so an entry point never leaves torch (or any other caller) on another device.
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err;
+  explicit DeviceGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    err = hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+#define SET_DEVICE(d)               \
+  fr::DeviceGuard dev_guard_((d));  \
+  HIPCHK(dev_guard_.err)
 
 constexpr uint32_t kBlock = 256;      // 4 waves, one 8x8 pixel tile each
 constexpr uint32_t kStripRows = 8;    // rows per shard strip == tile height
@@ -1496,7 +1517,33 @@ struct fr_ctx {
   uint32_t last_n = 0;
   bool pending = false;
   std::chrono::steady_clock::time_point t0;
+  // fr_ctx_trace_log: event pairs around every trace launch since the log was enabled,
+  // across renders (ev_trace holds only the last render's), so a caller streaming K
+  // frames can average the kernel's duration over all of them
+  // log 0: trace launches (on the launch's stream); log 1: whole renders (ev0 .. ev1)
+  bool log_on = false;
+  std::vector<hipEvent_t> log_ev[2];  // 2 per entry (start, end); reused across logs
+  size_t log_n[2] = {0, 0};           // entries logged
 };
+
+static hipError_t log_event(fr_ctx* c, int which, size_t k, hipStream_t st) {
+  std::vector<hipEvent_t>& v = c->log_ev[which];
+  while (v.size() <= k) {
+    hipEvent_t e;
+    const hipError_t err = hipEventCreate(&e);
+    if (err != hipSuccess) return err;
+    v.push_back(e);
+  }
+  return hipEventRecord(v[k], st);
+}
+static hipError_t log_start(fr_ctx* c, int which, hipStream_t st) {
+  return log_event(c, which, 2 * c->log_n[which], st);
+}
+static hipError_t log_end(fr_ctx* c, int which, hipStream_t st) {
+  const hipError_t e = log_event(c, which, 2 * c->log_n[which] + 1, st);
+  if (e == hipSuccess) ++c->log_n[which];
+  return e;
+}
 
 // Picks the specialisation: single-kind scenes (all boxes, all spheres) drop the
 // per-primitive kind switch; HAS_PLANE adds the stale-record bookkeeping; small depth
@@ -1518,6 +1565,8 @@ static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t 
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, static_cast<int>(kBlock), lds) != hipSuccess ||
       per_cu < 1)
     per_cu = 1;
+  // the per-wave counter slots (fr_ctx::d_wcnt) hold kMaxWgPerCu workgroups per CU
+  if (per_cu > static_cast<int>(kMaxWgPerCu)) per_cu = static_cast<int>(kMaxWgPerCu);
   const char* no_stage = getenv("FR_BVH_STAGE");  // "0": BVH kernels store unstaged (A/B, tests)
   if (g.stage_bytes && !(no_stage && strcmp(no_stage, "0") == 0)) {
     int staged = 0;
@@ -1635,7 +1684,7 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_error(FR_ENODEV, "no HIP device");
   if (device < 0 || device >= n) return set_error(FR_ENODEV, "device %d not present (%d devices)", device, n);
-  HIPCHK(hipSetDevice(device));
+  SET_DEVICE(device);
   fr_ctx* c = new fr_ctx();
   c->device = device;
   if (stream) {
@@ -1671,8 +1720,12 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
 
 void fr_ctx_free(fr_ctx* c) {
   if (!c) return;
+  int cur = -1;
+  (void)hipGetDevice(&cur);
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  // every stream drained before any buffer or event it may still use goes
+  for (hipStream_t s : {c->stream, c->stream2, c->stream_sum, c->stream_copy})
+    if (s) (void)hipStreamSynchronize(s);
   if (c->stream_copy) (void)hipStreamSynchronize(c->stream_copy), (void)hipStreamDestroy(c->stream_copy);
   if (c->ev_copy) (void)hipEventDestroy(c->ev_copy);
   if (c->d_mean) (void)hipFree(c->d_mean);
@@ -1683,6 +1736,8 @@ void fr_ctx_free(fr_ctx* c) {
   if (c->d_running) (void)hipFree(c->d_running);
   for (hipEvent_t e : c->ev_trace) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_sum) (void)hipEventDestroy(e);
+  for (auto& v : c->log_ev)
+    for (hipEvent_t e : v) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->stream2) (void)hipStreamSynchronize(c->stream2), (void)hipStreamDestroy(c->stream2);
   if (c->stream_sum) (void)hipStreamSynchronize(c->stream_sum), (void)hipStreamDestroy(c->stream_sum);
@@ -1690,13 +1745,14 @@ void fr_ctx_free(fr_ctx* c) {
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
+  if (cur >= 0) (void)hipSetDevice(cur);  // the caller's current device (torch's) stays as it was
 }
 
 int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_params* p) {
   if (!c || !scene || !cam) return set_error(FR_EARG, "fr_ctx_render: null argument");
   int rc = check_params(p);
   if (rc) return rc;
-  HIPCHK(hipSetDevice(c->device));
+  SET_DEVICE(c->device);
   DeviceCopy* dc = nullptr;
   rc = upload_scene(scene, c->device, &dc);
   if (rc) return rc;
@@ -1725,7 +1781,10 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   const float cam_reach = std::max(std::max(fabsf(cam->position[0]), fabsf(cam->position[1])),
                                    fabsf(cam->position[2])) + fabsf(cam->lens_radius);
   const bool cam_near = cam_reach <= kBvhOriginReach * (dc->bvh_extent + 1.0f);
-  const bool use_bvh = dc->bvh_ok && dc->n_segs > 0 && cam_near && !(bvh_env && strcmp(bvh_env, "0") == 0);
+  // save_image_mt renders run the in-order list kernels (launch_trace), whose LDS layout
+  // (sample staging, no traversal stack) the size below must follow
+  const bool use_bvh = dc->bvh_ok && dc->n_segs > 0 && cam_near && !(bvh_env && strcmp(bvh_env, "0") == 0) &&
+                       !(p->flags & FR_FLAG_MT_BANDS);
   ks.bvh = reinterpret_cast<const float4*>(b + dc->off_bvh);
   ks.bvh_order = reinterpret_cast<const uint32_t*>(b + dc->off_bvh_order);
   ks.lrec = reinterpret_cast<const float4*>(b + dc->off_lrec);
@@ -1853,6 +1912,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   }
 #endif
   HIPCHK(hipEventRecord(c->ev0, c->stream));
+  if (c->log_on) HIPCHK(log_start(c, 1, c->stream));
   HIPCHK(hipEventRecord(c->ev_start, c->stream));
   HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
   HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_start, 0));
@@ -1887,12 +1947,18 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
       kw.wave_counters = wcnt;
       HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), ts));
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced], ts));
+      if (c->log_on) HIPCHK(log_start(c, 0, ts));
       launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, grid, lds, ts, ks, kc, kp, kw);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced + 1], ts));
-      hipLaunchKernelGGL(reduce_counters, dim3(1), dim3(256), 0, ts, wcnt, blocks * (kBlock / 64u), c->d_cnt);
-      HIPCHK(hipGetLastError());
+      if (c->log_on) HIPCHK(log_end(c, 0, ts));
       HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_trace[2 * traced + 1], 0));
+      // on the sum stream, after the trace: the frame's end (ev1 on c->stream) waits for
+      // the sums, so fr_ctx_sync reads d_cnt after every pass's reduce, and the next
+      // frame's d_cnt memset (c->stream) cannot overtake a reduce of this one
+      hipLaunchKernelGGL(reduce_counters, dim3(1), dim3(256), 0, c->stream_sum, wcnt, blocks * (kBlock / 64u),
+                         c->d_cnt);
+      HIPCHK(hipGetLastError());
       ++traced;
     }
     const int first = pass == 0, last = pass + 1 >= passes;
@@ -1908,6 +1974,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   if (summed) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_sum[summed - 1], 0));
   c->passes = traced;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
+  if (c->log_on) HIPCHK(log_end(c, 1, c->stream));
   c->last = *p;
   c->last_n = dc->n;
   c->pending = true;
@@ -1916,7 +1983,7 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
 
 int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
   if (!c) return set_error(FR_EARG, "fr_ctx_sync: null ctx");
-  HIPCHK(hipSetDevice(c->device));
+  SET_DEVICE(c->device);
   HIPCHK(hipStreamSynchronize(c->stream));
   if (!c->pending) return set_error(FR_EARG, "fr_ctx_sync: nothing rendered");
   if (st) {
@@ -2051,7 +2118,7 @@ static int enqueue_download(fr_ctx* c, hipStream_t st, float* mean_rgb, uint8_t*
 
 int fr_ctx_download(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
   if (!c || !c->pending) return set_error(FR_EARG, "fr_ctx_download: nothing rendered");
-  HIPCHK(hipSetDevice(c->device));
+  SET_DEVICE(c->device);
   const int rc = enqueue_download(c, c->stream, mean_rgb, rgb8);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -2060,7 +2127,7 @@ int fr_ctx_download(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
 
 int fr_ctx_download_async(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
   if (!c || !c->pending) return set_error(FR_EARG, "fr_ctx_download_async: nothing rendered");
-  HIPCHK(hipSetDevice(c->device));
+  SET_DEVICE(c->device);
   HIPCHK(hipStreamWaitEvent(c->stream_copy, c->ev1, 0));  // after the last render's sum
   const int rc = enqueue_download(c, c->stream_copy, mean_rgb, rgb8);
   if (rc) return rc;
@@ -2071,7 +2138,7 @@ int fr_ctx_download_async(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
 
 int fr_ctx_wait(fr_ctx* c) {
   if (!c) return set_error(FR_EARG, "fr_ctx_wait: null ctx");
-  HIPCHK(hipSetDevice(c->device));
+  SET_DEVICE(c->device);
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->stream2));
   HIPCHK(hipStreamSynchronize(c->stream_sum));
@@ -2112,57 +2179,191 @@ int fr_render_hip(fr_scene* scene, const fr_camera* cam, const fr_params* params
   return rc;
 }
 
+int fr_ctx_trace_log(fr_ctx* c, int enable) {
+  if (!c) return set_error(FR_EARG, "fr_ctx_trace_log: null ctx");
+  if (enable) {
+    SET_DEVICE(c->device);
+    // the pairs of an earlier log may still be pending on the streams: drain them before
+    // their events are recorded again
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream2));
+    c->log_n[0] = c->log_n[1] = 0;
+  }
+  c->log_on = enable != 0;
+  return FR_OK;
+}
+
+int fr_ctx_trace_log_read(fr_ctx* c, int which, double* ms, uint32_t cap, uint32_t* n) {
+  if (!c || !n || which < 0 || which > 1) return set_error(FR_EARG, "fr_ctx_trace_log_read: bad argument");
+  SET_DEVICE(c->device);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream2));
+  *n = static_cast<uint32_t>(c->log_n[which]);
+  for (size_t i = 0; i < c->log_n[which] && i < cap && ms; ++i) {
+    float t = 0.0f;
+    HIPCHK(hipEventElapsedTime(&t, c->log_ev[which][2 * i], c->log_ev[which][2 * i + 1]));
+    ms[i] = t;
+  }
+  return FR_OK;
+}
+
+}  // extern "C"
+
+// ---- multi-device context (render_mt's row tiling over devices, tracer.rs:83-134) ----
+// One fr_ctx per entry of the device list (duplicates allowed: two contexts on one device
+// rehearse a two-device run), each rendering shard i of n of every frame; the shards'
+// strips land in one page-locked host frame by asynchronous D2H copies, one per context.
+// Everything is allocated at creation or on a frame of a larger size; a frame of the same
+// size allocates nothing.
+struct fr_mctx {
+  std::vector<fr_ctx*> ctx;
+  float* h_mean = nullptr;  // pinned full frame: W x H x 3 f32, then W x H x 3 u8
+  uint8_t* h_u8 = nullptr;
+  size_t cap_pixels = 0;
+  uint32_t width = 0, height = 0;
+  bool pending = false;
+  std::chrono::steady_clock::time_point t0;
+};
+
+extern "C" {
+
+void fr_mctx_free(fr_mctx* m) {
+  if (!m) return;
+  for (fr_ctx* c : m->ctx) fr_ctx_free(c);  // each drains its streams first
+  if (m->h_mean) (void)hipHostFree(m->h_mean);
+  delete m;
+}
+
+int fr_mctx_create(const int* devices, int n, fr_mctx** out) {
+  if (!devices || n < 1 || !out) return set_error(FR_EARG, "fr_mctx_create: bad arguments");
+  *out = nullptr;
+  fr_mctx* m = new fr_mctx();
+  for (int i = 0; i < n; ++i) {
+    fr_ctx* c = nullptr;
+    const int rc = fr_ctx_create(devices[i], nullptr, &c);
+    if (rc) {
+      const std::string msg = fr_last_error();
+      fr_mctx_free(m);
+      return set_error(rc, "fr_mctx_create: entry %d (device %d): %s", i, devices[i], msg.c_str());
+    }
+    m->ctx.push_back(c);
+  }
+  *out = m;
+  return FR_OK;
+}
+
+int fr_mctx_count(const fr_mctx* m) { return m ? static_cast<int>(m->ctx.size()) : 0; }
+
+int fr_mctx_ctx(fr_mctx* m, int i, fr_ctx** out) {
+  if (!m || !out || i < 0 || i >= static_cast<int>(m->ctx.size())) return set_error(FR_EARG, "fr_mctx_ctx: bad index");
+  *out = m->ctx[i];
+  return FR_OK;
+}
+
+int fr_mctx_render(fr_mctx* m, fr_scene* scene, const fr_camera* cam, const fr_params* params) {
+  if (!m || !scene || !cam || !params) return set_error(FR_EARG, "fr_mctx_render: null argument");
+  const int n = static_cast<int>(m->ctx.size());
+  fr_params p = *params;
+  p.shard_count = static_cast<uint32_t>(n);
+  p.shard_index = 0;
+  int rc = check_params(&p);
+  if (rc) return rc;
+  const size_t pixels = static_cast<size_t>(p.width) * p.height;
+  if (pixels > m->cap_pixels) {
+    // a larger frame: the previous frame's gathers may still write the old host frame
+    for (fr_ctx* c : m->ctx)
+      if ((rc = fr_ctx_wait(c))) return rc;
+    if (m->h_mean) HIPCHK(hipHostFree(m->h_mean));
+    m->h_mean = nullptr;
+    m->h_u8 = nullptr;
+    m->cap_pixels = 0;
+    void* h = nullptr;
+    HIPCHK(hipHostMalloc(&h, pixels * 3 * (sizeof(float) + 1), hipHostMallocDefault));
+    m->h_mean = static_cast<float*>(h);
+    m->h_u8 = reinterpret_cast<uint8_t*>(m->h_mean + pixels * 3);
+    m->cap_pixels = pixels;
+  }
+  m->width = p.width;
+  m->height = p.height;
+  m->t0 = std::chrono::steady_clock::now();
+  // enqueue every shard and its gather, then return: the devices run concurrently
+  for (int i = 0; i < n; ++i) {
+    p.shard_index = static_cast<uint32_t>(i);
+    if ((rc = fr_ctx_render(m->ctx[i], scene, cam, &p))) return set_error(rc, "shard %d: %s", i, fr_last_error());
+    if ((rc = fr_ctx_download_async(m->ctx[i], m->h_mean, (p.flags & FR_FLAG_WRITE_U8) ? m->h_u8 : nullptr)))
+      return set_error(rc, "shard %d: %s", i, fr_last_error());
+  }
+  m->pending = true;
+  return FR_OK;
+}
+
+int fr_mctx_sync(fr_mctx* m, fr_stats* stats) {
+  if (!m) return set_error(FR_EARG, "fr_mctx_sync: null mctx");
+  if (!m->pending) return set_error(FR_EARG, "fr_mctx_sync: nothing rendered");
+  fr_stats agg;
+  memset(&agg, 0, sizeof(agg));
+  for (size_t i = 0; i < m->ctx.size(); ++i) {
+    fr_stats st;
+    int rc = fr_ctx_sync(m->ctx[i], &st);
+    if (!rc) rc = fr_ctx_wait(m->ctx[i]);  // the shard's gather has landed
+    if (rc) return set_error(rc, "shard %zu: %s", i, fr_last_error());
+    agg.segments += st.segments;
+    agg.hits += st.hits;
+    agg.samples += st.samples;
+    agg.prim_tests += st.prim_tests;
+    agg.scatters += st.scatters;
+    agg.kernel_ms = std::max(agg.kernel_ms, st.kernel_ms);  // the slowest shard
+    agg.trace_ms = std::max(agg.trace_ms, st.trace_ms);
+    agg.trace_launches = std::max(agg.trace_launches, st.trace_launches);
+    agg.occupancy = st.occupancy;
+  }
+  agg.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - m->t0).count();
+  if (stats) *stats = agg;
+  return FR_OK;
+}
+
+int fr_mctx_frame(fr_mctx* m, const float** mean_rgb, const uint8_t** rgb8) {
+  if (!m || !m->pending) return set_error(FR_EARG, "fr_mctx_frame: nothing rendered");
+  if (mean_rgb) *mean_rgb = m->h_mean;
+  if (rgb8) *rgb8 = m->h_u8;
+  return FR_OK;
+}
+
+int fr_mctx_download(fr_mctx* m, float* mean_rgb, uint8_t* rgb8) {
+  if (!m || !m->pending) return set_error(FR_EARG, "fr_mctx_download: nothing rendered");
+  for (fr_ctx* c : m->ctx) {
+    const int rc = fr_ctx_wait(c);
+    if (rc) return rc;
+  }
+  const size_t n = static_cast<size_t>(m->width) * m->height * 3;
+  if (mean_rgb) memcpy(mean_rgb, m->h_mean, n * sizeof(float));
+  if (rgb8) memcpy(rgb8, m->h_u8, n);
+  return FR_OK;
+}
+
 int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* params, int n_gpus,
                         float* mean_rgb, uint8_t* rgb8, fr_stats* stats) {
   if (!params || n_gpus < 1) return set_error(FR_EARG, "fr_render_hip_multi: bad arguments");
   int avail = 0;
   if (hipGetDeviceCount(&avail) != hipSuccess || avail < n_gpus)
     return set_error(FR_ENODEV, "fr_render_hip_multi: %d devices requested, %d present", n_gpus, avail);
-  // Upload on the calling thread first so the per-device threads only read the scene.
-  for (int g = 0; g < n_gpus; ++g) {
-    HIPCHK(hipSetDevice(g));
-    DeviceCopy* dc = nullptr;
-    const int rc = upload_scene(scene, g, &dc);
-    if (rc) return rc;
-  }
-  std::vector<int> rcs(n_gpus, 0);
-  std::vector<fr_stats> sts(n_gpus);
-  std::vector<std::string> errs(n_gpus);
-  const auto t0 = std::chrono::steady_clock::now();
-  std::vector<std::thread> th;
-  for (int g = 0; g < n_gpus; ++g) {
-    th.emplace_back([&, g]() {
-      fr_params p = *params;
-      p.shard_index = static_cast<uint32_t>(g);
-      p.shard_count = static_cast<uint32_t>(n_gpus);
-      rcs[g] = fr_render_hip(scene, cam, &p, g, mean_rgb, rgb8, &sts[g]);
-      if (rcs[g]) errs[g] = fr_last_error();
-    });
-  }
-  for (auto& t : th) t.join();
-  for (int g = 0; g < n_gpus; ++g)
-    if (rcs[g]) return set_error(rcs[g], "device %d: %s", g, errs[g].c_str());
-  if (stats) {
-    memset(stats, 0, sizeof(*stats));
-    for (int g = 0; g < n_gpus; ++g) {
-      stats->segments += sts[g].segments;
-      stats->hits += sts[g].hits;
-      stats->samples += sts[g].samples;
-      stats->prim_tests += sts[g].prim_tests;
-      if (sts[g].kernel_ms > stats->kernel_ms) stats->kernel_ms = sts[g].kernel_ms;
-      if (sts[g].trace_ms > stats->trace_ms) stats->trace_ms = sts[g].trace_ms;
-      if (sts[g].trace_launches > stats->trace_launches) stats->trace_launches = sts[g].trace_launches;
-      stats->scatters += sts[g].scatters;
-      stats->occupancy = sts[g].occupancy;
-    }
-    stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  }
-  return FR_OK;
+  std::vector<int> devs(n_gpus);
+  for (int g = 0; g < n_gpus; ++g) devs[g] = g;
+  fr_mctx* m = nullptr;
+  int rc = fr_mctx_create(devs.data(), n_gpus, &m);
+  if (rc) return rc;
+  fr_params p = *params;
+  if (rgb8) p.flags |= FR_FLAG_WRITE_U8;
+  rc = fr_mctx_render(m, scene, cam, &p);
+  if (!rc) rc = fr_mctx_sync(m, stats);
+  if (!rc) rc = fr_mctx_download(m, mean_rgb, rgb8);
+  fr_mctx_free(m);
+  return rc;
 }
 
 int fr_selftest_ops(int device, int op, const float* a, const float* b, uint32_t n, float* out) {
   if (!a || !b || !out) return set_error(FR_EARG, "fr_selftest_ops: null buffer");
-  HIPCHK(hipSetDevice(device));
+  SET_DEVICE(device);
   float *da = nullptr, *db = nullptr, *dout = nullptr;
   const size_t bytes = (n ? n : 1) * sizeof(float);
   HIPCHK(hipMalloc(&da, bytes));
@@ -2181,7 +2382,7 @@ int fr_selftest_ops(int device, int op, const float* a, const float* b, uint32_t
 
 int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
   if (!out) return set_error(FR_EARG, "fr_selftest_rng: null buffer");
-  HIPCHK(hipSetDevice(device));
+  SET_DEVICE(device);
   uint32_t* d = nullptr;
   HIPCHK(hipMalloc(&d, (n ? n : 1) * sizeof(uint32_t)));
   hipLaunchKernelGGL(rng_kernel, dim3(1), dim3(64), 0, 0, seed, pixel, sample, n, d);
@@ -2195,7 +2396,7 @@ int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, 
    bad[256] / first[256] per exponent field (first = 0xFFFFFFFF when none). */
 int fr_selftest_recip(int device, uint64_t base, uint64_t count, uint64_t* bad, uint32_t* first) {
   if (!bad || !first || base + count > (1ull << 32)) return set_error(FR_EARG, "fr_selftest_recip: bad arguments");
-  HIPCHK(hipSetDevice(device));
+  SET_DEVICE(device);
   unsigned long long* dbad = nullptr;
   uint32_t* dfirst = nullptr;
   HIPCHK(hipMalloc(&dbad, 256 * sizeof(unsigned long long)));

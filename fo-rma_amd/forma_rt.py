@@ -27,7 +27,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FORMA_RT_LIB") or os.path.join(HERE, "libforma_rt.so")
 SCENES_DIR = os.path.join(HERE, "scenes")
 
-FR_ABI_VERSION = 3  # include/forma_rt.h FR_ABI_VERSION
+FR_ABI_VERSION = 4  # include/forma_rt.h FR_ABI_VERSION
 FR_OK, FR_EARG, FR_EPARSE, FR_EHIP, FR_ENODEV, FR_ENOMEM = 0, -1, -2, -3, -4, -5
 FR_SPHERE, FR_PLANE, FR_AABB, FR_OBB, FR_STUB, FR_TRIANGLE = 0, 1, 2, 3, 4, 5
 FR_LAMBERTIAN, FR_METAL, FR_DIELECTRIC, FR_LIGHT = 0, 1, 2, 3
@@ -82,7 +82,9 @@ EXPORTS = (
     "fr_scene_get_prims", "fr_scene_translate", "fr_scene_rotate",
     "fr_camera_init", "fr_camera_look", "fr_camera_orbit", "fr_camera_translate", "fr_update_delta",
     "fr_ctx_create", "fr_ctx_free", "fr_ctx_render", "fr_ctx_sync", "fr_ctx_download", "fr_ctx_download_async",
-    "fr_ctx_wait", "fr_ctx_device_buffers", "fr_host_alloc", "fr_host_free",
+    "fr_ctx_wait", "fr_ctx_device_buffers", "fr_host_alloc", "fr_host_free", "fr_ctx_trace_log",
+    "fr_ctx_trace_log_read", "fr_mctx_create", "fr_mctx_free", "fr_mctx_count", "fr_mctx_ctx", "fr_mctx_render",
+    "fr_mctx_sync", "fr_mctx_frame", "fr_mctx_download",
     "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_recip",
     "fr_post_process", "fr_post_process_device", "fr_rgb_to_rgba_device",
 )
@@ -145,6 +147,18 @@ def lib():
         L.fr_host_alloc.argtypes = [C.c_size_t, P(vp)]
         L.fr_host_free.argtypes = [vp]
         L.fr_host_free.restype = None
+    if hasattr(L, "fr_mctx_create"):  # absent from A/B builds of older sources
+        L.fr_ctx_trace_log.argtypes = [vp, C.c_int]
+        L.fr_ctx_trace_log_read.argtypes = [vp, C.c_int, P(C.c_double), C.c_uint32, P(C.c_uint32)]
+        L.fr_mctx_create.argtypes = [P(C.c_int), C.c_int, P(vp)]
+        L.fr_mctx_free.argtypes = [vp]
+        L.fr_mctx_free.restype = None
+        L.fr_mctx_count.argtypes = [vp]
+        L.fr_mctx_ctx.argtypes = [vp, C.c_int, P(vp)]
+        L.fr_mctx_render.argtypes = [vp, vp, P(FrCamera), P(FrParams)]
+        L.fr_mctx_sync.argtypes = [vp, P(FrStats)]
+        L.fr_mctx_frame.argtypes = [vp, P(P(C.c_float)), P(P(C.c_uint8))]
+        L.fr_mctx_download.argtypes = [vp, f3, P(C.c_uint8)]
     L.fr_render_hip.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
     L.fr_render_hip_multi.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
     L.fr_selftest_ops.argtypes = [C.c_int, C.c_int, f3, f3, C.c_uint32, f3]
@@ -385,23 +399,47 @@ def make_params(width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, shar
     return p
 
 
+class _PinnedBlock:
+    """One fr_host_alloc allocation. Freed when the last reference goes: every numpy view
+    made by _pinned_views holds one (through its ctypes buffer), so an array a caller kept
+    never points at freed memory."""
+
+    def __init__(self, nbytes):
+        self.ptr = C.c_void_p()
+        check(lib().fr_host_alloc(max(1, nbytes), C.byref(self.ptr)))
+        self.nbytes = nbytes
+
+    def __del__(self):
+        try:
+            if self.ptr and self.ptr.value:
+                lib().fr_host_free(self.ptr)
+                self.ptr = C.c_void_p()
+        except Exception:
+            pass
+
+
+def _pinned_views(block, width, height):
+    n = width * height * 3
+    buf = (C.c_uint8 * block.nbytes).from_address(block.ptr.value)
+    buf._owner = block  # the buffer (the arrays' base) keeps the allocation alive
+    mean = np.frombuffer(buf, dtype=np.float32, count=n).reshape(height, width, 3)
+    u8 = np.frombuffer(buf, dtype=np.uint8, count=n, offset=n * 4).reshape(height, width, 3)
+    return mean, u8
+
+
 class PinnedFrame:
     """Full-image host buffers in page-locked memory (fr_host_alloc): mean [H, W, 3] f32
-    and u8 [H, W, 3], the targets of RenderContext.download_async."""
+    and u8 [H, W, 3], the targets of RenderContext.download_async. close() drops the
+    frame's own views; the memory is returned once no view of it is left anywhere."""
 
     def __init__(self, width, height):
-        n = width * height * 3
-        self._p = C.c_void_p()
-        check(lib().fr_host_alloc(n * 5, C.byref(self._p)))
-        buf = (C.c_uint8 * (n * 5)).from_address(self._p.value)
-        self.mean = np.frombuffer(buf, dtype=np.float32, count=n).reshape(height, width, 3)
-        self.u8 = np.frombuffer(buf, dtype=np.uint8, count=n, offset=n * 4).reshape(height, width, 3)
+        self.width, self.height = width, height
+        self._block = _PinnedBlock(width * height * 3 * 5)
+        self.mean, self.u8 = _pinned_views(self._block, width, height)
 
     def close(self):
-        if self._p and self._p.value:
-            self.mean = self.u8 = None
-            lib().fr_host_free(self._p)
-            self._p = C.c_void_p()
+        self.mean = self.u8 = None
+        self._block = None
 
     def __del__(self):
         try:
@@ -451,6 +489,20 @@ class RenderContext:
         """Block until every render and download enqueued on this context has finished."""
         check(lib().fr_ctx_wait(self._h))
 
+    def trace_log(self, enable=True):
+        """Start (or stop) logging every trace-kernel launch's HIP-event duration."""
+        check(lib().fr_ctx_trace_log(self._h, 1 if enable else 0))
+
+    def trace_log_read(self, frames=False):
+        """HIP-event durations (ms) logged since trace_log(True): every trace-kernel launch,
+        or (frames=True) every whole render (trace + sum kernels)."""
+        which = 1 if frames else 0
+        n = C.c_uint32(0)
+        check(lib().fr_ctx_trace_log_read(self._h, which, None, 0, C.byref(n)))
+        arr = (C.c_double * max(1, n.value))()
+        check(lib().fr_ctx_trace_log_read(self._h, which, arr, n.value, C.byref(n)))
+        return [arr[i] for i in range(n.value)]
+
     def device_buffers(self):
         """(d_mean_rgb, d_rgb8) device addresses of the last render's full-image outputs."""
         dm, du = C.c_void_p(), C.c_void_p()
@@ -458,8 +510,68 @@ class RenderContext:
         return dm.value, du.value
 
     def close(self):
+        if getattr(self, "_borrowed", False):
+            return
         if self._h and self._h.value:
             lib().fr_ctx_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiContext:
+    """fr_mctx: one fr_ctx per entry of `devices` (entries may repeat), shard i of n of
+    every frame on entry i, the strips gathered asynchronously into one page-locked host
+    frame. Persistent: frames of the same size allocate nothing (tracer.rs:83-134's row
+    tiling, one device per shard instead of one thread)."""
+
+    def __init__(self, devices):
+        devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+        self._h = C.c_void_p()
+        check(lib().fr_mctx_create(devs, len(devices), C.byref(self._h)))
+        self.devices = list(devices)
+        self._shape = None
+
+    def render(self, scene, cam, params):
+        """Enqueue one frame (all shards and their gathers); returns at once."""
+        check(lib().fr_mctx_render(self._h, scene._h, C.byref(cam), C.byref(params)))
+        self._shape = (params.height, params.width, 3)
+
+    def sync(self):
+        st = FrStats()
+        check(lib().fr_mctx_sync(self._h, C.byref(st)))
+        return st.as_dict()
+
+    def frame(self):
+        """(mean, u8) numpy copies of the host frame of the last render (after sync)."""
+        fp, up = C.POINTER(C.c_float)(), C.POINTER(C.c_uint8)()
+        check(lib().fr_mctx_frame(self._h, C.byref(fp), C.byref(up)))
+        n = self._shape[0] * self._shape[1] * 3
+        mean = np.ctypeslib.as_array(fp, shape=(n,)).reshape(self._shape).copy()
+        u8 = np.ctypeslib.as_array(up, shape=(n,)).reshape(self._shape).copy()
+        return mean, u8
+
+    def frame_ptrs(self):
+        """Host addresses of the page-locked frame (mean, u8)."""
+        fp, up = C.POINTER(C.c_float)(), C.POINTER(C.c_uint8)()
+        check(lib().fr_mctx_frame(self._h, C.byref(fp), C.byref(up)))
+        return C.cast(fp, C.c_void_p).value, C.cast(up, C.c_void_p).value
+
+    def context(self, i):
+        """The i-th shard's RenderContext view (not owned: do not close it)."""
+        h = C.c_void_p()
+        check(lib().fr_mctx_ctx(self._h, i, C.byref(h)))
+        rc = RenderContext.__new__(RenderContext)
+        rc._h, rc.device, rc._borrowed = h, self.devices[i], True
+        return rc
+
+    def close(self):
+        if self._h and self._h.value:
+            lib().fr_mctx_free(self._h)
             self._h = C.c_void_p()
 
     def __del__(self):
@@ -541,7 +653,9 @@ class TraceModel:
     def frame_u8(self, scene, max_depth, seed):
         """update()'s frame: 1 spp, only the u8 image copied back, by DMA into page-locked
         memory that `pixels` views (overwritten by the next frame, as tracer.rs's
-        model.pixels is)."""
+        model.pixels is). The view keeps the page-locked block alive, so an array returned
+        here stays valid memory after the model is closed or collected; copy it to keep a
+        frame past the next update()."""
         ctx = self.context()
         ctx.render(scene, self.scene.camera, make_params(self.width, self.height, 1, max_depth, seed))
         self.last_stats = ctx.sync()
@@ -553,7 +667,8 @@ class TraceModel:
 
     def close(self):
         if self._pinned is not None:
-            self.pixels = np.array(self.pixels)  # keep the last frame past the pinned buffer
+            # model.pixels (and any array update() returned) keeps the page-locked block
+            # alive by itself; only the model's own frame object goes
             self._pinned.close()
             self._pinned = None
         if self.ctx is not None:

@@ -28,8 +28,10 @@
  *   fr_update_delta .................. cpu_ray_tracer/tracer.rs:30-52 (update's key bitmask)
  *   fr_ctx_render / fr_render_hip .... cpu_ray_tracer/tracer.rs:160-219 (save_image +
  *                                      get_color) and tracer.rs:57-81 (render, 1 spp)
- *   fr_render_hip_multi .............. tracer.rs:83-134 (render_mt row tiling), one
- *                                      device per row shard instead of one thread
+ *   fr_mctx_* / fr_render_hip_multi .. tracer.rs:83-134 (render_mt row tiling), one
+ *                                      device per row shard instead of one thread;
+ *                                      fr_mctx keeps the per-device contexts and a
+ *                                      page-locked frame across renders (update loop)
  *
  * Errors: 0 = ok, negative = FR_E*; the message is in fr_last_error() (thread-local).
  * Threading: calls on distinct fr_scene / fr_ctx objects are re-entrant. A fr_ctx is
@@ -45,9 +47,11 @@
 extern "C" {
 #endif
 
-#define FR_ABI_VERSION 3 /* 2: fr_stats.trace_launches; FR_TRIANGLE; post effects; FR_FLAG_MT_BANDS
+#define FR_ABI_VERSION 4 /* 2: fr_stats.trace_launches; FR_TRIANGLE; post effects; FR_FLAG_MT_BANDS
                             3: fr_stats.scatters/.occupancy; fr_ctx_download_async, fr_ctx_wait,
-                               fr_host_alloc/free; item-major sample buffer */
+                               fr_host_alloc/free; item-major sample buffer
+                            4: fr_mctx_* (persistent multi-device context); fr_ctx_trace_log(_read);
+                               entry points restore the caller's current HIP device */
 
 /* error codes */
 #define FR_OK 0
@@ -149,6 +153,7 @@ typedef struct fr_stats {
 
 typedef struct fr_scene fr_scene; /* opaque: host primitive list + per-device copies */
 typedef struct fr_ctx fr_ctx;     /* opaque: one device, one stream, output buffers */
+typedef struct fr_mctx fr_mctx;   /* opaque: one fr_ctx per device entry + a page-locked host frame */
 
 /* ---- library ---- */
 const char* fr_last_error(void);
@@ -196,6 +201,33 @@ int fr_ctx_download_async(fr_ctx* ctx, float* mean_rgb, uint8_t* rgb8);
 int fr_ctx_wait(fr_ctx* ctx);
 /* Device pointers of the last render's full-image output buffers. */
 int fr_ctx_device_buffers(fr_ctx* ctx, float** d_mean_rgb, uint8_t** d_rgb8);
+/* Launch log: enable != 0 starts a new log (previous entries dropped); every later render
+   records HIP events around each trace-kernel launch (on the launch's stream) and around
+   the whole render (trace + sum kernels). _read waits for the logged work and writes up
+   to cap durations (ms) in order: which = 0 the trace launches, 1 the renders; *n = the
+   entries logged. Lets a caller streaming K frames average all K of them. */
+int fr_ctx_trace_log(fr_ctx* ctx, int enable);
+int fr_ctx_trace_log_read(fr_ctx* ctx, int which, double* ms, uint32_t cap, uint32_t* n);
+
+/* ---- persistent multi-device context (tracer.rs:83-134 render_mt, one device per shard) ----
+   Entry i of `devices` renders row shard i of n of every frame on its own fr_ctx (device
+   entries may repeat). Contexts, device buffers and the page-locked host frame persist
+   across renders; a frame no larger than the last allocates nothing. */
+int fr_mctx_create(const int* devices, int n, fr_mctx** out);
+void fr_mctx_free(fr_mctx* mctx);
+int fr_mctx_count(const fr_mctx* mctx);
+/* The i-th shard's context (owned by the mctx). */
+int fr_mctx_ctx(fr_mctx* mctx, int i, fr_ctx** out);
+/* Enqueue one frame: every shard's render, then its asynchronous gather into the host
+   frame; returns at once. params' shard fields are ignored (shard i of n). The u8 image
+   is gathered when params->flags has FR_FLAG_WRITE_U8. */
+int fr_mctx_render(fr_mctx* mctx, fr_scene* scene, const fr_camera* cam, const fr_params* params);
+/* Wait for every shard and gather; stats summed over shards (times: the slowest shard). */
+int fr_mctx_sync(fr_mctx* mctx, fr_stats* stats);
+/* The page-locked host frame (W*H*3 f32 means, W*H*3 u8), valid until the next render. */
+int fr_mctx_frame(fr_mctx* mctx, const float** mean_rgb, const uint8_t** rgb8);
+/* Wait, then copy the host frame into caller buffers (either may be NULL). */
+int fr_mctx_download(fr_mctx* mctx, float* mean_rgb, uint8_t* rgb8);
 
 /* Page-locked host memory (hipHostMalloc) for fr_ctx_download_async targets. */
 int fr_host_alloc(size_t bytes, void** out);
@@ -205,7 +237,7 @@ void fr_host_free(void* p);
 /* One shard on one device; writes the shard's rows into caller-owned host buffers. */
 int fr_render_hip(fr_scene* scene, const fr_camera* cam, const fr_params* params, int device,
                   float* mean_rgb, uint8_t* rgb8, fr_stats* stats);
-/* The whole image row-sharded across devices 0..n_gpus-1 (one host thread + stream each). */
+/* The whole image row-sharded across devices 0..n_gpus-1: an fr_mctx created, used once and freed. */
 int fr_render_hip_multi(fr_scene* scene, const fr_camera* cam, const fr_params* params, int n_gpus,
                         float* mean_rgb, uint8_t* rgb8, fr_stats* stats);
 

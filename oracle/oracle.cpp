@@ -737,6 +737,11 @@ int oracle_closest_hit(const or_prim* prims, uint32_t n, const float o[3], const
 // (1 = all). Parallel over `threads` in chunks of 32 pixels of a row (the render_mt
 // shape, tracer.rs:83-134, without its per-pixel scene rebuild). Writes means and u8
 // for the pixels it renders; returns the number of rows.
+int64_t oracle_render_rows(const or_prim* prims, uint32_t n, const or_camera* cam, uint32_t width, uint32_t height,
+                           uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* row_list,
+                           uint32_t n_rows, uint32_t col_step, int threads, float* out_mean, uint8_t* out_u8,
+                           or_counters* counters);
+
 int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, uint32_t width, uint32_t height,
                       uint32_t spp, uint32_t max_depth, uint64_t seed, uint32_t shard_index, uint32_t shard_count,
                       uint32_t row_step, uint32_t col_step, int threads, float* out_mean, uint8_t* out_u8,
@@ -744,15 +749,28 @@ int64_t oracle_render(const or_prim* prims, uint32_t n, const or_camera* cam, ui
   if (!cam || width == 0 || height == 0 || shard_count == 0 || shard_index >= shard_count || row_step == 0 ||
       col_step == 0)
     return -1;
-  const auto objects = build(prims, n);
-  Camera camera;
-  camera.from_c(cam);
   std::vector<uint32_t> rows;
   uint32_t kept = 0;
   for (uint32_t y = 0; y < height; ++y) {
     if ((y / 8) % shard_count != shard_index) continue;
     if (kept++ % row_step == 0) rows.push_back(y);
   }
+  return oracle_render_rows(prims, n, cam, width, height, spp, max_depth, seed, rows.data(),
+                            static_cast<uint32_t>(rows.size()), col_step, threads, out_mean, out_u8, counters);
+}
+
+// The same loop over an explicit list of image rows (each < height).
+int64_t oracle_render_rows(const or_prim* prims, uint32_t n, const or_camera* cam, uint32_t width, uint32_t height,
+                           uint32_t spp, uint32_t max_depth, uint64_t seed, const uint32_t* row_list,
+                           uint32_t n_rows, uint32_t col_step, int threads, float* out_mean, uint8_t* out_u8,
+                           or_counters* counters) {
+  if (!cam || width == 0 || height == 0 || col_step == 0 || (n_rows && !row_list)) return -1;
+  for (uint32_t i = 0; i < n_rows; ++i)
+    if (row_list[i] >= height) return -1;
+  const std::vector<uint32_t> rows(row_list, row_list + n_rows);
+  const auto objects = build(prims, n);
+  Camera camera;
+  camera.from_c(cam);
   const uint32_t cols = (width + col_step - 1) / col_step;  // pixels x = 0, col_step, ...
   const uint32_t chunk = 32, chunks = (cols + chunk - 1) / chunk;
   if (threads < 1) threads = 1;

@@ -53,6 +53,10 @@ def lib():
                                     C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                     C.c_uint32, C.c_int, f3, C.POINTER(C.c_uint8), C.POINTER(OrCounters)]
         L.oracle_render.restype = C.c_int64
+        L.oracle_render_rows.argtypes = [C.POINTER(OrPrim), C.c_uint32, C.POINTER(OrCamera), C.c_uint32, C.c_uint32,
+                                         C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint32,
+                                         C.c_uint32, C.c_int, f3, C.POINTER(C.c_uint8), C.POINTER(OrCounters)]
+        L.oracle_render_rows.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -145,6 +149,36 @@ def render(prims, cam, width, height, spp, max_depth, seed=0x5EED, shard_index=0
         raise ValueError("oracle_render: bad arguments")
     return mean, u8, {"segments": cnt.segments, "hits": cnt.hits, "samples": cnt.samples,
                       "scatters": cnt.scatters}, int(rows)
+
+
+def render_rows(prims, cam, width, height, spp, max_depth, rows, seed=0x5EED, threads=1, col_step=1, chunk=None,
+                progress=None, out=None):
+    """save_image semantics on an explicit list of image rows, rendered `chunk` rows per
+    oracle call (progress(done, total) after each). out=(mean, u8, counters) continues
+    filling earlier results. Returns (mean, u8, counters dict)."""
+    if out is None:
+        mean = np.full((height, width, 3), np.nan, dtype=np.float32)
+        u8 = np.zeros((height, width, 3), dtype=np.uint8)
+        tot = {"segments": 0, "hits": 0, "samples": 0, "scatters": 0}
+    else:
+        mean, u8, tot = out
+    rows = [int(r) for r in rows]
+    chunk = chunk or max(1, len(rows))
+    pc = prims_to_c(prims)
+    for i in range(0, len(rows), chunk):
+        part = rows[i:i + chunk]
+        arr = (C.c_uint32 * len(part))(*part)
+        cnt = OrCounters()
+        r = lib().oracle_render_rows(pc, len(prims), C.byref(cam), width, height, spp, max_depth, seed, arr, len(part),
+                                     col_step, threads, mean.ctypes.data_as(C.POINTER(C.c_float)),
+                                     u8.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(cnt))
+        if r < 0:
+            raise ValueError("oracle_render_rows: bad arguments")
+        for k in tot:
+            tot[k] += getattr(cnt, k)
+        if progress:
+            progress(min(i + chunk, len(rows)), len(rows))
+    return mean, u8, tot
 
 
 def render_mt(prims, cam, width, height, sample, max_depth=50, seed=0x5EED):

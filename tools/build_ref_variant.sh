@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build libforma_rt from the kernel sources of a git revision, for A/B timing against the
 # working tree (tools/ab_bench.py):
-#   tools/build_ref_variant.sh REV NAME [DEFS]  ->  fo-rma_amd/build/variants/libforma_rt_NAME.so
+#   tools/build_ref_variant.sh REV NAME [DEFS]  ->  fo-rma_amd/build/ab/libforma_rt_NAME.so (shipped to the GPU box; delete after the A/B session)
 # REV "." takes the working tree's sources (for -D variants of uncommitted code).
 # The host objects (scene, JSON, BVH, post) come from the working tree's build; the ABI of
 # REV must match the working tree's include/forma_rt.h.
@@ -17,11 +17,11 @@ else
   git -C "$root" archive "$rev" fo-rma_amd/csrc include | tar -x -C "$tmp"
 fi
 make -C "$root/fo-rma_amd" -s build/scene.o build/json_min.o build/bvh.o build/post.o
-mkdir -p "$root/fo-rma_amd/build/variants"
+mkdir -p "$root/fo-rma_amd/build/ab"
 FP="-ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP -fno-slp-vectorize $defs \
   -c "$tmp/fo-rma_amd/csrc/render.hip" -o "$tmp/render.o"
 b="$root/fo-rma_amd/build"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$b/variants/libforma_rt_$name.so" "$tmp/render.o" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$b/ab/libforma_rt_$name.so" "$tmp/render.o" \
   "$b/scene.o" "$b/json_min.o" "$b/bvh.o" "$b/post.o"
-echo "$b/variants/libforma_rt_$name.so"
+echo "$b/ab/libforma_rt_$name.so"
