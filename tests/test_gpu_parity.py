@@ -826,8 +826,9 @@ def test_pass_pipeline_never_changes_results(gpu, pipe, buf_gb, monkeypatch):
 @pytest.mark.slow
 @pytest.mark.parametrize("shard,buf_gb", [(0, "8"), (7, None)])
 def test_c4_shards_on_row_subsets(gpu, shard, buf_gb, monkeypatch):
-    """C4 (scene_08 3840x2160, 1024 spp, 8 bounces) as ranks 0 and 7 of 8 render it: 27 of
-    the shard's 270 rows (every 10th), all 3,840 pixels each, against the oracle. Shard 0
+    """C4 (scene_08 3840x2160, 1024 spp, 8 bounces) as ranks 0 and 7 of 8 render it: every
+    10th row of the shard (28 of shard 0's 272 rows, 27 of shard 7's 264), all 3,840 pixels
+    each, against the oracle. Shard 0
     runs with an 8-GB sample buffer (passes of 21 of its 64 blocks), shard 7 in one pass."""
     if buf_gb:
         monkeypatch.setenv("FR_SAMPLE_BUFFER_GB", buf_gb)
@@ -840,7 +841,7 @@ def test_c4_shards_on_row_subsets(gpu, shard, buf_gb, monkeypatch):
     prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path("scene_08")).read())
     cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
     rows = mine[::10]
-    assert len(rows) == 27
+    assert len(rows) >= 27
     omean, ou8, _ = O.render_rows(prims, cam, w, h, spp, depth, rows, threads=oracle_threads(), chunk=9,
                                   progress=_progress(f"C4 shard {shard}"))
     assert_parity(mean, u8, st, omean, ou8, None, rows=rows)
