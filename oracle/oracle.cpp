@@ -523,7 +523,10 @@ struct Camera {
   }
 };
 
-struct Counters {
+// one cache line per thread's counters: they are bumped on every segment, and adjacent
+// per-thread counters would share lines between cores (false sharing cost the threaded
+// oracle about 3x at 16 threads)
+struct alignas(64) Counters {
   uint64_t segments = 0, hits = 0, scatters = 0;
 };
 
@@ -777,7 +780,7 @@ int64_t oracle_render_rows(const or_prim* prims, uint32_t n, const or_camera* ca
   std::atomic<size_t> next{0};
   std::vector<Counters> cnts(threads);
   auto work = [&](int tid) {
-    Counters& cnt = cnts[tid];
+    Counters cnt;  // thread-local while rendering, stored once at the end
     for (size_t wi; (wi = next.fetch_add(1)) < rows.size() * chunks;) {
       const uint32_t y = rows[wi / chunks];
       const uint32_t c0 = static_cast<uint32_t>(wi % chunks) * chunk;
@@ -810,6 +813,7 @@ int64_t oracle_render_rows(const or_prim* prims, uint32_t n, const or_camera* ca
         }
       }
     }
+    cnts[tid] = cnt;
   };
   std::vector<std::thread> pool;
   for (int t = 1; t < threads; ++t) pool.emplace_back(work, t);
