@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <string>
 #include <thread>
+#include <type_traits>
 
 #include "bvh.h"
 #include "internal.h"
@@ -116,6 +117,7 @@ constexpr uint32_t KF_STAGE = 1u << 30;            // internal: BVH kernel stage
 constexpr uint32_t kNibbleMaxPrims = 15;
 constexpr uint32_t kNibbleUnit = 15;
 constexpr uint32_t KF_NIBBLE = 1u << 29;           // internal: 8-B deferred records
+constexpr uint32_t KF_DIFFUSE = 1u << 28;          // internal: no metal/dielectric (trace_kernel MAT = 1)
 #ifndef FR_BLOCK_SAMPLES
 #define FR_BLOCK_SAMPLES 16  // RNG contract: one stream per 16-sample block (oracle.cpp agrees)
 #endif
@@ -152,11 +154,13 @@ struct DeviceCopy {
   uint32_t kinds = 0;  // bit k set if a primitive of kind k is present
   size_t off_mat = 0, off_cls = 0, off_att = 0;
   size_t off_rec = 0;
-  size_t off_bvh = 0, off_bvh_order = 0, off_lrec = 0, off_segs = 0;
+  size_t off_bvh = 0, off_bvh_order = 0, off_lrec = 0, off_segs = 0, off_runs = 0;
+  uint32_t n_runs = 0;
   bool bvh_ok = false;  // segments and trees built (else the in-order loop only)
   float bvh_extent = 0; // largest |coordinate| of the primitives' bounds (bvh.h)
   uint32_t n_segs = 0;  // closest-hit segments: BVH runs and planes (bvh.h)
   bool att_nonneg = true;  // every attenuation component finite and >= +0 (no -0)
+  bool diffuse = true;     // no metal or dielectric scatter class (trace_kernel MAT = 1)
 };
 
 struct KScene {
@@ -170,6 +174,10 @@ struct KScene {
   const uint32_t* __restrict__ bvh_order;  // primitive index of each leaf slot
   const float4* __restrict__ lrec;  // the primitives' records in leaf-slot order
   const uint4* __restrict__ segs;   // BvhSegment list: runs (one tree each) and planes, in list order
+  // kind runs of the list (KS_ANY in-order loop): {kind, first, end, 0} for each maximal run
+  // of consecutive primitives of one kind, in list order
+  const uint4* __restrict__ runs;
+  uint32_t n_runs;
   uint32_t n;
   uint32_t n_segs;                  // segment count (0: no BVH)
   uint32_t att_nonneg;              // every attenuation component finite and >= +0
@@ -410,7 +418,9 @@ enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 // amdgpu_num_sgpr caps the scalar registers (MI355X_MICROARCH.md "Residency and
 // cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
 // admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
-template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, int DEFER>
+// MAT = 1: no metal or dielectric primitive (every scatter is lambertian: lambertian, light,
+// or none for stubs): the shading step drops those branches (the headline scene's case).
+template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, int DEFER, int MAT = 0>
 // Waves per SIMD the kernels ask for: the list-loop kernels at least 7 (<= 72 VGPRs), the
 // BVH kernels at least 6 (<= 80); without the request the general (KS_ANY) and BVH
 // kernels settle at 83-94 VGPRs, 5 waves. Measured (tools/ab_bench.py): 7 for the list
@@ -441,6 +451,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   extern __shared__ uint32_t lds[];
   constexpr uint32_t STG = stage_samples(BVH);
   constexpr bool NIB = DEFER == 2;             // 8-B records, winners in a register
+  constexpr bool DIFFUSE = MAT == 1;           // lambertian scatters only
   constexpr uint32_t WPS = NIB ? 2u : 3u;      // words per sample in the buffer
   // list kernels always stage; BVH kernels when the launch gave them the LDS (KF_STAGE)
   const bool staged = STG > 1 && (!BVH || (kp.flags & KF_STAGE) != 0u);
@@ -735,7 +746,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           const V3 r{px, py, pz};
           bool ok = true;
           V3 dir;
-          if (smetal) {
+          if (!DIFFUSE && smetal) {
             dir = add(d, scl(sfuzz, r));  // reflected + fuzz * rus
             ok = dot(dir, sn) > 0.0f;     // sphere.rs:104 / plane.rs:121
           } else {
@@ -887,27 +898,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           }
         }
       }
-      for (uint32_t ii = 0; ii < (list_walk ? sc.n : 0u); ++ii) {
-        // the index is wave-uniform; say so, or the compiler may fall back to vector loads
-        const uint32_t i = __builtin_amdgcn_readfirstlane(ii);
+      // one primitive of kind K at list index i (wave-uniform): records by scalar loads
+      auto test_one = [&](auto kind_tag, uint32_t i) {
+        constexpr uint32_t K = decltype(kind_tag)::value;
         const RecRef r4 = rec_at(sc.rec, i);  // scalar loads
-        const uint32_t k = KS == KS_AABB ? FR_AABB
-                           : KS == KS_SPHERE ? FR_SPHERE
-                                             : __float_as_uint(r4[3].w);  // scalar branch
         float t = 0.0f;
         bool h = false;
-        if (k == FR_AABB) {
+        if constexpr (K == FR_AABB) {
           h = slab_root(slab3(xyz(r4[0]), xyz(r4[1]), o, inv), 0.001f, closest, t);
-        } else if (k == FR_SPHERE) {
+        } else if constexpr (K == FR_SPHERE) {
           const float4 g = r4[0];
           h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, closest, t);
-        } else if (k == FR_PLANE) {
+        } else if constexpr (K == FR_PLANE) {
           const int r = plane_test(xyz(r4[0]), xyz(r4[1]), xyz(r4[2]), o, d, 0.001f, closest, t);
           if (r) t_last = t;
           h = r == 2;
-        } else if (k == FR_TRIANGLE) {
+        } else if constexpr (K == FR_TRIANGLE) {
           h = tri_root(xyz(r4[0]), xyz(r4[1]), xyz(r4[2]), o, d, 0.001f, closest, t);
-        } else if (k == FR_OBB) {
+        } else if constexpr (K == FR_OBB) {
           const float4 a = r4[0], b = r4[1], c = r4[2], e = r4[3];
           const ObbFrame f = obb_frame(xyz(a), xyz(b), xyz(c), xyz(e), o, d);
           h = slab_root(slab3(V3{-a.w, -b.w, -c.w}, V3{a.w, b.w, c.w}, f.ol, f.inv), 0.001f, closest, t);
@@ -916,6 +924,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           closest = t;
           best = static_cast<int>(i);
           if (HAS_PLANE) t_last = t;
+        }
+      };
+      typedef std::integral_constant<uint32_t, FR_AABB> TagAabb;
+      typedef std::integral_constant<uint32_t, FR_SPHERE> TagSphere;
+      if constexpr (KS != KS_ANY) {
+        for (uint32_t ii = 0; ii < (list_walk ? sc.n : 0u); ++ii) {
+          // the index is wave-uniform; say so, or the compiler may fall back to vector loads
+          const uint32_t i = __builtin_amdgcn_readfirstlane(ii);
+          if constexpr (KS == KS_AABB)
+            test_one(TagAabb{}, i);
+          else
+            test_one(TagSphere{}, i);
+        }
+      } else {
+        // The list in order, as its kind runs: one scalar kind branch per run instead of a
+        // dependent kind load and branch per primitive, and a tight loop per run whose
+        // record loads do not wait on a kind test (the same tests in the same order).
+        typedef __attribute__((address_space(4))) const uint32_t cu32r;
+        for (uint32_t rr = 0; rr < (list_walk ? sc.n_runs : 0u); ++rr) {
+          const cu32r* rp = (cu32r*)(reinterpret_cast<uintptr_t>(sc.runs)) + 4u * __builtin_amdgcn_readfirstlane(rr);
+          const uint32_t k = rp[0], i0 = rp[1], i1 = rp[2];
+          if (k == FR_AABB) {
+            for (uint32_t i = i0; i < i1; ++i) test_one(TagAabb{}, __builtin_amdgcn_readfirstlane(i));
+          } else if (k == FR_SPHERE) {
+            for (uint32_t i = i0; i < i1; ++i) test_one(TagSphere{}, __builtin_amdgcn_readfirstlane(i));
+          } else if (k == FR_PLANE) {
+            for (uint32_t i = i0; i < i1; ++i)
+              test_one(std::integral_constant<uint32_t, FR_PLANE>{}, __builtin_amdgcn_readfirstlane(i));
+          } else if (k == FR_TRIANGLE) {
+            for (uint32_t i = i0; i < i1; ++i)
+              test_one(std::integral_constant<uint32_t, FR_TRIANGLE>{}, __builtin_amdgcn_readfirstlane(i));
+          } else if (k == FR_OBB) {
+            for (uint32_t i = i0; i < i1; ++i)
+              test_one(std::integral_constant<uint32_t, FR_OBB>{}, __builtin_amdgcn_readfirstlane(i));
+          }  // FR_STUB: never hits (aabb.rs:21-34, rectangle.rs:21-34)
         }
       }
       PROF_MARK(PF_HIT);
@@ -950,7 +993,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
             b2 = buf_load4(sc.rec, off + 32u);
             b3 = buf_load4(sc.rec, off + 48u);
           }
-          const uint32_t c = n_att ? __float_as_uint(att_lds[best].w) : buf_load1(sc.cls, 4u * best);
+          // (a single-kind scene has no stubs: with DIFFUSE every class scatters lambertian)
+          const uint32_t c = (DIFFUSE && KS != KS_ANY) ? static_cast<uint32_t>(SC_LAMBERT)
+                             : n_att                   ? __float_as_uint(att_lds[best].w)
+                                                       : buf_load1(sc.cls, 4u * best);
           const uint32_t kb = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(b3.w);
           V3 n;
           if (kb == FR_AABB) {
@@ -976,10 +1022,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           o = p;
           d = add(p, n);  // lambertian / light: target = (p + n) + rus
           sbest = static_cast<uint32_t>(best);
-          smetal = c == SC_METAL;
+          smetal = !DIFFUSE && c == SC_METAL;
           ended = c == SC_NONE;
-          if (c != SC_NONE && c != SC_DIELECTRIC) need = NEED_SPHERE;
-          if (c == SC_DIELECTRIC) {
+          if (c != SC_NONE && (DIFFUSE || c != SC_DIELECTRIC)) need = NEED_SPHERE;
+          if (!DIFFUSE && c == SC_DIELECTRIC) {
             // one draw, no rejection loop (sphere.rs:107-145)
             d = scatter_dielectric(din, n, rng);
             push(static_cast<uint32_t>(best));
@@ -1383,11 +1429,25 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   off = align_up(off + (bvh_order.size() ? bvh_order.size() : 1) * 64, 256);
   c->off_segs = off;
   off = align_up(off + (bvh_segs.size() ? bvh_segs.size() : 1) * sizeof(BvhSegment), 256);
+  // kind runs: maximal runs of consecutive primitives of one kind, in list order
+  std::vector<uint32_t> runs;
+  for (uint32_t i = 0; i < n;) {
+    const uint32_t k = s->prims[i].kind <= FR_TRIANGLE ? s->prims[i].kind : FR_STUB;
+    uint32_t j = i + 1;
+    while (j < n && (s->prims[j].kind <= FR_TRIANGLE ? s->prims[j].kind : FR_STUB) == k) ++j;
+    runs.insert(runs.end(), {k, i, j, 0u});
+    i = j;
+  }
+  c->n_runs = static_cast<uint32_t>(runs.size() / 4);
+  c->off_runs = off;
+  off = align_up(off + (runs.size() ? runs.size() : 4) * 4, 256);
   std::vector<unsigned char> host(off, 0);
   bool nonneg = true;
+  bool diffuse = true;
   if (!bvh_nodes.empty()) memcpy(&host[c->off_bvh], bvh_nodes.data(), bvh_nodes.size() * sizeof(BvhNode));
   if (!bvh_order.empty()) memcpy(&host[c->off_bvh_order], bvh_order.data(), bvh_order.size() * 4);
   if (!bvh_segs.empty()) memcpy(&host[c->off_segs], bvh_segs.data(), bvh_segs.size() * sizeof(BvhSegment));
+  if (!runs.empty()) memcpy(&host[c->off_runs], runs.data(), runs.size() * 4);
   c->bvh_ok = bvh_ok;
   c->bvh_extent = bvh_extent;
   c->n_segs = static_cast<uint32_t>(bvh_segs.size());
@@ -1427,6 +1487,7 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
       default: kind = FR_STUB;
     }
     const uint32_t cls = scatter_class(p);
+    if (cls == SC_METAL || cls == SC_DIELECTRIC) diffuse = false;
     const float4 mat = make_float4(p.color[0], p.color[1], p.color[2], p.fuzz);
     const float4 att = cls == SC_LIGHT ? make_float4(1.0f, 1.0f, 1.0f, 0.0f)
                                        : make_float4(p.color[0], p.color[1], p.color[2], 0.0f);
@@ -1439,6 +1500,7 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
     memcpy(&host[c->off_rec + 64 * i], g, 64);
   }
   c->att_nonneg = nonneg;
+  c->diffuse = diffuse;
   // the BVH leaves' records, in leaf-slot order
   for (size_t slot = 0; slot < bvh_order.size(); ++slot)
     memcpy(&host[c->off_lrec + 64 * slot], &host[c->off_rec + 64 * static_cast<size_t>(bvh_order[slot])], 64);
@@ -1594,7 +1656,10 @@ static void launch_depth(bool small_depth, const Grid& g, size_t lds, hipStream_
                          const KCam& kc, const KParams& kp, const KWork& kw) {
   if constexpr (!BV && !MT) {
     if (kp.flags & KF_DEFER) {
-      if (kp.flags & KF_NIBBLE)
+      if ((kp.flags & KF_NIBBLE) && (kp.flags & KF_DIFFUSE))
+        launch_persistent(trace_kernel<KS, HP, FR_KREJ_NIB, kSmallDepth, false, false, 2, 1>, g, lds, st,
+                          KArgs{ks, kc, kp, kw});
+      else if (kp.flags & KF_NIBBLE)
         launch_persistent(trace_kernel<KS, HP, FR_KREJ_NIB, kSmallDepth, false, false, 2>, g, lds, st,
                           KArgs{ks, kc, kp, kw});
       else
@@ -1789,6 +1854,8 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   ks.bvh_order = reinterpret_cast<const uint32_t*>(b + dc->off_bvh_order);
   ks.lrec = reinterpret_cast<const float4*>(b + dc->off_lrec);
   ks.segs = reinterpret_cast<const uint4*>(b + dc->off_segs);
+  ks.runs = reinterpret_cast<const uint4*>(b + dc->off_runs);
+  ks.n_runs = dc->n_runs;
   ks.n_segs = use_bvh ? dc->n_segs : 0u;
   ks.reach = kBvhOriginReach * (dc->bvh_extent + 1.0f);
   ks.att_nonneg = dc->att_nonneg ? 1u : 0u;
@@ -1834,6 +1901,9 @@ int fr_ctx_render(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const fr_par
   const bool nibble = defer && dc->n <= kNibbleMaxPrims && !(defer_env && strcmp(defer_env, "1") == 0);
   if (defer) kp.flags |= KF_DEFER;
   if (nibble) kp.flags |= KF_NIBBLE;
+  // FR_MAT=0 keeps the general shading step for diffuse-only scenes (A/B, tests)
+  const char* mat_env = getenv("FR_MAT");
+  if (dc->diffuse && !(mat_env && strcmp(mat_env, "0") == 0)) kp.flags |= KF_DIFFUSE;
   const uint32_t wps = nibble ? 2u : 3u;  // words per sample in the buffer
   const size_t per_block = static_cast<size_t>(kp.P) * kp.ks * wps * sizeof(float);
   uint32_t want_passes = 1;

@@ -251,6 +251,23 @@ def test_random_scenes_all_kinds_and_materials(gpu, seed):
     assert_parity(mean, u8, st, omean, ou8, ocnt)
 
 
+@pytest.mark.parametrize("seed", [2, 3, 4, 5])
+def test_diffuse_only_scenes(gpu, seed):
+    """Scenes without metal or dielectric run the diffuse-only shading step (trace_kernel
+    MAT = 1) — here the general-kind kernel with planes, stubs, triangles and light (whose
+    attenuation is 1, sphere.rs:147-152) — against the oracle."""
+    w, h, spp, depth = 40, 24, 4, 8
+    prims = random_scene(seed)
+    for q in prims:
+        if q["material"] in (S.METAL, S.DIELECTRIC):
+            q["material"] = S.LIGHT if seed % 2 else S.LAMBERTIAN
+    assert len(prims) <= 15
+    sc = gpu.Scene.from_prims(prims)
+    mean, u8, st = gpu.render(sc, gpu.camera_new(w, h), w, h, spp, depth, seed=300 + seed)
+    omean, ou8, ocnt, _ = O.render(prims, O.camera_new(w, h), w, h, spp, depth, seed=300 + seed, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+
+
 @pytest.mark.parametrize("shards", [2, 3, 8])
 def test_row_shards_stitch_bit_exactly(gpu, shards):
     w, h, spp, depth = 100, 50, 4, 8  # H % 8 != 0: last strip is partial
@@ -696,7 +713,8 @@ def test_bvh_generator_10k_spheres_small(gpu, depth):
 def test_record_formats_are_bit_identical(gpu, scene, spp, monkeypatch):
     """The deferred unwind stores 8-B records (4-bit winners) for scenes of <= 15
     primitives and 12-B records (u8 winners) above; FR_DEFER=1 forces the 12-B form and
-    FR_DEFER=0 the unwind in the trace kernel. All three give the same bits."""
+    FR_DEFER=0 the unwind in the trace kernel; FR_MAT=0 the general shading step where a
+    scene has no metal or dielectric (scene_08). All give the same bits."""
     w, h = 48, 32
     if scene == "random":
         prims = [p for p in random_scene(5) if p["kind"] != S.PLANE]
@@ -707,11 +725,13 @@ def test_record_formats_are_bit_identical(gpu, scene, spp, monkeypatch):
         cam = sc.camera
     assert len(sc) <= 15
     monkeypatch.delenv("FR_DEFER", raising=False)
+    monkeypatch.delenv("FR_MAT", raising=False)
     ref = gpu.render(sc, cam, w, h, spp, 8)
-    for mode in ("1", "0"):
-        monkeypatch.setenv("FR_DEFER", mode)
+    for env in (("FR_DEFER", "1"), ("FR_DEFER", "0"), ("FR_MAT", "0")):
+        monkeypatch.delenv("FR_DEFER", raising=False)
+        monkeypatch.setenv(*env)
         mean, u8, st = gpu.render(sc, cam, w, h, spp, 8)
-        assert np.array_equal(mean.view(np.uint32), ref[0].view(np.uint32)) and np.array_equal(u8, ref[1]), mode
+        assert np.array_equal(mean.view(np.uint32), ref[0].view(np.uint32)) and np.array_equal(u8, ref[1]), env
         assert (st["segments"], st["hits"], st["scatters"]) == (ref[2]["segments"], ref[2]["hits"], ref[2]["scatters"])
 
 
