@@ -434,7 +434,11 @@ template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, int DEF
 // 20.49 ms and shard 0/4 -0.6 % (shard 0/8 +0.3 %); at KREJ 4 it had measured -0.3 % / +1.1 %
 #define FR_NIB_WAVES 8
 #endif
-#define FR_OCC_ATTR __attribute__((amdgpu_waves_per_eu(BVH ? 6 : DEFER == 2 ? FR_NIB_WAVES : 7)))
+#ifndef FR_DIFF12_WAVES
+#define FR_DIFF12_WAVES 7  // diffuse-only 12-B-record kernels (A/B knob)
+#endif
+#define FR_OCC_ATTR \
+  __attribute__((amdgpu_waves_per_eu(BVH ? 6 : DEFER == 2 ? FR_NIB_WAVES : (DEFER == 1 && MAT == 1) ? FR_DIFF12_WAVES : 7)))
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) FR_OCC_ATTR void trace_kernel(
     KArgs args) {
@@ -456,9 +460,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // list kernels always stage; BVH kernels when the launch gave them the LDS (KF_STAGE)
   const bool staged = STG > 1 && (!BVH || (kp.flags & KF_STAGE) != 0u);
   float* stage = reinterpret_cast<float*>(lds) + threadIdx.x * (WPS * STG);
-  const uint32_t n_att = sc.n <= kAttLds ? sc.n : 0u;
+  // DEFER kernels (<= kDeferMaxPrims primitives) always hold the attenuations in LDS, and
+  // the 8-B-record kernels (<= kNibbleMaxPrims) the records too: compile-time facts there,
+  // so their global-load fallbacks are not compiled
+  constexpr bool ATT_LDS = DEFER != 0, REC_LDS = NIB;
+  static_assert(kDeferMaxPrims <= kAttLds && kNibbleMaxPrims <= kRecLds, "LDS staging bounds");
+  const uint32_t n_att = ATT_LDS || sc.n <= kAttLds ? sc.n : 0u;
   const uint32_t n_att_st = n_att ? n_att + 1u : 0u;  // with the unit entry
-  const uint32_t n_rec = sc.n <= kRecLds ? sc.n : 0u;
+  const uint32_t n_rec = REC_LDS || sc.n <= kRecLds ? sc.n : 0u;
   float4* att_lds = reinterpret_cast<float4*>(lds + (staged ? kBlock * WPS * STG : 0u));
   float4* rec_lds = att_lds + n_att_st;
   uint32_t* stack = reinterpret_cast<uint32_t*>(rec_lds + 4u * n_rec);
@@ -980,7 +989,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           // the winner's record and class: LDS when staged (n_rec / n_att are uniform;
           // separate branches keep LDS and global reads in their own address spaces)
           float4 b0, b1, b2, b3;
-          if (n_rec) {
+          if (REC_LDS || n_rec) {
             const float4* rb = rec_lds + 4 * best;
             b0 = rb[0];
             b1 = rb[1];
@@ -995,7 +1004,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           }
           // (a single-kind scene has no stubs: with DIFFUSE every class scatters lambertian)
           const uint32_t c = (DIFFUSE && KS != KS_ANY) ? static_cast<uint32_t>(SC_LAMBERT)
-                             : n_att                   ? __float_as_uint(att_lds[best].w)
+                             : ATT_LDS || n_att        ? __float_as_uint(att_lds[best].w)
                                                        : buf_load1(sc.cls, 4u * best);
           const uint32_t kb = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(b3.w);
           V3 n;
@@ -1661,6 +1670,9 @@ static void launch_depth(bool small_depth, const Grid& g, size_t lds, hipStream_
                           KArgs{ks, kc, kp, kw});
       else if (kp.flags & KF_NIBBLE)
         launch_persistent(trace_kernel<KS, HP, FR_KREJ_NIB, kSmallDepth, false, false, 2>, g, lds, st,
+                          KArgs{ks, kc, kp, kw});
+      else if (kp.flags & KF_DIFFUSE)
+        launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, false, false, 1, 1>, g, lds, st,
                           KArgs{ks, kc, kp, kw});
       else
         launch_persistent(trace_kernel<KS, HP, FR_KREJ, kSmallDepth, false, false, 1>, g, lds, st,
