@@ -95,6 +95,14 @@ constexpr uint32_t kMaxWgPerCu = 8;   // 2048 threads per CU / kBlock: the persi
 #ifndef FR_KREJ_NIB
 #define FR_KREJ_NIB 6
 #endif
+#ifndef FR_CLAIM_MIN
+#define FR_CLAIM_MIN 1  // lanes that must wait for an item before the wave claims (tuning only)
+#endif
+// ... for the 8-B-record kernels (the headline's): C3 18.50 -> 18.28 ms at 2 (18.31 at 4, 18.46
+// at 6); 4 on every kernel cost C2 +2 %, so the others keep FR_CLAIM_MIN
+#ifndef FR_CLAIM_MIN_NIB
+#define FR_CLAIM_MIN_NIB 2
+#endif
 #ifndef FR_NUM_SGPR
 #define FR_NUM_SGPR 96
 #endif
@@ -585,7 +593,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     ++diag_iter;
 #endif
     const unsigned long long m = __ballot(need_item);
-    if (m) {
+    // Lanes whose item is done wait (idle) until FR_CLAIM_MIN of them need one, or until no
+    // active lane has other work: the claim step (its lane permutes and item setup) then
+    // runs for several lanes at once instead of in nearly every iteration for one or two.
+    // Only when work starts changes, never what a sample computes (results bit-identical).
+    constexpr uint32_t CLAIM_MIN = NIB ? FR_CLAIM_MIN_NIB : FR_CLAIM_MIN;
+    if (m && (CLAIM_MIN <= 1 || lanes_set(need_item) >= CLAIM_MIN || m == __ballot(1))) {
       // 0. claim work items: the free lanes take consecutive items of the wave's batch;
       // when it runs out, the first free lane reserves the next batch of kBatch = 64
       // items (one tile of one sample block) globally. n <= 64, so one batch suffices.
