@@ -986,7 +986,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       PROF_MARK(PF_HIT);
       if (best < 0) {
         if (DEFER)
+#ifdef FR_FAST_SKY
+          tsky = __float_as_uint(sky_t_fast(d));  // tracer.rs:211-218, the blend in sum_kernel
+#else
           tsky = __float_as_uint(sky_t(d));  // tracer.rs:211-218, the blend in sum_kernel
+#endif
         else
           term = sky(d);  // tracer.rs:211-218
         ended = true;
@@ -1366,6 +1370,12 @@ __global__ void ops_kernel(int op, const float* a, const float* b, uint32_t n, f
     case 11: r = fmax3_num(x, y, b[(i + 1) % n]); break;  // vs fmaxf(fmaxf(x, y), z)
     case 12: r = fmin_num(fmin_num(x, y), b[(i + 1) % n]); break;
     case 13: r = fmax_num(fmax_num(x, y), b[(i + 1) % n]); break;  // chained v_max_f32
+    case 14: {  // sky_t_fast against sky_t on the direction (x, y, z = b[i + 1]): 0 when equal bits
+      const V3 dv{x, y, b[(i + 1) % n]};
+      r = __uint_as_float(__float_as_uint(sky_t_fast(dv)) ^ __float_as_uint(sky_t(dv)));
+      break;
+    }
+    case 15: r = sky_t_fast(V3{x, y, b[(i + 1) % n]}); break;
     default: r = 0.0f;
   }
   out[i] = r;

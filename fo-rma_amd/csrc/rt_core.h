@@ -322,12 +322,27 @@ FR_HD V3 axis_normal(int k, float s) {
 // Outward normal of the accepted root t (t == tn: entry face, else exit face), in the
 // frame whose ray direction is dd.
 FR_HD V3 slab_normal(const Slab& s, float t, V3 dd) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // Branch-free form of the two cases below, for t == tn or t == tf (slab_root's roots;
+  // the caller recomputes the winner's slab with the same operations): entry iff t == tn;
+  // the first axis whose near (entry) or far (exit) distance equals t; the sign is
+  // -sign(d_k) on entry and +sign(d_k) on exit, sign(0) counted negative. Selects on lane
+  // masks instead of a divergent branch in which both cases ran for a mixed wave.
+  const bool entry = t == s.tn;
+  const bool kx = entry ? fmin_num(s.t0.x, s.t1.x) == t : fmax_num(s.t0.x, s.t1.x) == t;
+  const bool ky = !kx && (entry ? fmin_num(s.t0.y, s.t1.y) == t : fmax_num(s.t0.y, s.t1.y) == t);
+  const bool kz = !kx && !ky;
+  const float dk = kx ? dd.x : (ky ? dd.y : dd.z);
+  const float sg = ((dk > 0.0f) != entry) ? 1.0f : -1.0f;
+  return V3{kx ? sg : 0.0f, ky ? sg : 0.0f, kz ? sg : 0.0f};
+#else
   if (t == s.tn) {
     const int k = fmin_num(s.t0.x, s.t1.x) == s.tn ? 0 : (fmin_num(s.t0.y, s.t1.y) == s.tn ? 1 : 2);
     return axis_normal(k, comp(dd, k) > 0.0f ? -1.0f : 1.0f);
   }
   const int k = fmax_num(s.t0.x, s.t1.x) == s.tf ? 0 : (fmax_num(s.t0.y, s.t1.y) == s.tf ? 1 : 2);
   return axis_normal(k, comp(dd, k) > 0.0f ? 1.0f : -1.0f);
+#endif
 }
 
 // Build-defined triangle: Moller-Trumbore in f32 with this order;
@@ -424,6 +439,36 @@ FR_HD float sky_t(V3 d) {
 }
 FR_HD V3 sky_from_t(float t) { return add(scl(1.0f - t, V3{1.0f, 1.0f, 1.0f}), scl(t, V3{0.5f, 0.7f, 1.0f})); }
 FR_HD V3 sky(V3 d) { return sky_from_t(sky_t(d)); }
+
+#if defined(__HIP__)
+// sky_t (tracer.rs:211-218's blend parameter 0.5 (unit(d).y + 1)) with the correctly
+// rounded sqrt and division done by their core sequences where the operands allow it:
+// v_sqrt_f32 and the compiler's two FMA residual corrections without the denormal
+// scaling and class fix-up (identities for dd in [2^-96, 2^126]); and d.y / len by
+// div_rn(d.y, len, recip_nr(len)) (recip_nr exact for len's exponent range there, div_rn's
+// steps identities for |d.y| in {0} u [2^-100, 2^100]; a quotient below 2^-26, where the
+// core sequence could differ in the denormal range, gives 1 + q = 1 either way). Other
+// lanes take the plain expression. Bit-identical to sky_t: fr_selftest_ops op 14.
+__device__ __forceinline__ float sky_t_fast(V3 d) {
+  const float dd = d.x * d.x + d.y * d.y + d.z * d.z;  // length()'s sum, in its order
+  const float ay = __builtin_fabsf(d.y);
+  const bool fast = (dd >= 0x1p-96f) & (dd <= 0x1p126f) & ((ay >= 0x1p-100f) | (ay == 0.0f));
+  if (fast) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float s = __builtin_amdgcn_sqrtf(dd);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sup = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rdn = __builtin_fmaf(-sdn, s, dd);
+    const float rup = __builtin_fmaf(-sup, s, dd);
+    float len = rdn <= 0.0f ? sdn : s;
+    len = rup > 0.0f ? sup : len;
+    const float q = div_rn(d.y, len, recip_nr(len));
+    return 0.5f * (q + 1.0f);
+#endif
+  }
+  return sky_t(d);
+}
+#endif
 
 // tracer.rs:182-184: Rust `as u8` saturates (NaN -> 0) and truncates toward zero.
 FR_HD uint8_t to_u8(float c) {

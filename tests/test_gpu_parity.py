@@ -145,6 +145,28 @@ def test_guarded_recip_and_jitter_division(gpu):
         assert _same_bits(out, a / b), wh
 
 
+def test_fast_sky_parameter_is_bit_identical(gpu):
+    """sky_t_fast (the sky blend parameter with guarded core sqrt/division sequences,
+    render.hip FR_FAST_SKY) against the plain correctly rounded sky_t on the device, bit for
+    bit (op 14 returns the XOR of both results' bits), over random directions of every scale
+    and the guards' edges: tiny, zero, -0, denormal and huge components."""
+    import ctypes as C
+    rng = np.random.default_rng(14)
+    fp = C.POINTER(C.c_float)
+    n = 400000
+    scale = (2.0 ** rng.uniform(-70, 70, (3, n))).astype(np.float32)
+    v = (rng.standard_normal((3, n)).astype(np.float32) * scale).astype(np.float32)
+    edges = np.array([0.0, -0.0, 1e-45, -1e-45, 2.0 ** -100, -(2.0 ** -100), 2.0 ** -101, 2.0 ** -60, 2.0 ** -48,
+                      2.0 ** -47, 2.0 ** 62, 2.0 ** 63, 2.0 ** 64, 1.0, -1.0, 3e-39, 1e-30], dtype=np.float32)
+    e = np.array(np.meshgrid(edges, edges, edges)).reshape(3, -1)
+    v = np.concatenate([v, e, e[[1, 2, 0]]], axis=1).astype(np.float32)
+    x, y = np.ascontiguousarray(v[0]), np.ascontiguousarray(v[1])  # z of lane i is y[i + 1] (op 14)
+    out = np.empty_like(x)
+    gpu.check(gpu.lib().fr_selftest_ops(0, 14, x.ctypes.data_as(fp), y.ctypes.data_as(fp), x.size,
+                                        out.ctypes.data_as(fp)))
+    assert not out.view(np.uint32).any(), int(np.count_nonzero(out.view(np.uint32)))
+
+
 def test_device_schlick_unit_and_u8_match_oracle(gpu):
     import ctypes as C
     rng = np.random.default_rng(2)
