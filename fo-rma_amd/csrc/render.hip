@@ -793,7 +793,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       // of each test is needed here; the record is formed for the winner below.
       ++nseg;
       V3 inv{recip_nr(d.x), recip_nr(d.y), recip_nr(d.z)};
-      if (!(recip_nr_ok(d.x) && recip_nr_ok(d.y) && recip_nr_ok(d.z))) inv = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+      // (non-short-circuit: one branch to the rare fallback instead of three nested ones)
+      const int rok = static_cast<int>(recip_nr_ok(d.x)) & static_cast<int>(recip_nr_ok(d.y)) &
+                      static_cast<int>(recip_nr_ok(d.z));
+      if (!rok) inv = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
       const float a_dd = dot(d, d);
       float closest = FLT_MAX, t_last = 0.0f;
       int best = -1;
@@ -950,6 +953,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       };
       typedef std::integral_constant<uint32_t, FR_AABB> TagAabb;
       typedef std::integral_constant<uint32_t, FR_SPHERE> TagSphere;
+#ifdef FR_UNROLL_NIB
+      if constexpr (NIB && KS != KS_ANY) {
+        // <= kNibbleMaxPrims primitives: the loop unrolled, so every index is an immediate
+        // (the winner select needs no copy of the index into a VGPR) and the next record's
+        // scalar loads can be issued ahead
+#pragma unroll
+        for (uint32_t i = 0; i < kNibbleMaxPrims; ++i) {
+          if (i >= sc.n) break;
+          if constexpr (KS == KS_AABB)
+            test_one(TagAabb{}, i);
+          else
+            test_one(TagSphere{}, i);
+        }
+      } else
+#endif
       if constexpr (KS != KS_ANY) {
         for (uint32_t ii = 0; ii < (list_walk ? sc.n : 0u); ++ii) {
           // the index is wave-uniform; say so, or the compiler may fall back to vector loads
