@@ -953,11 +953,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       };
       typedef std::integral_constant<uint32_t, FR_AABB> TagAabb;
       typedef std::integral_constant<uint32_t, FR_SPHERE> TagSphere;
-#ifdef FR_UNROLL_NIB
+#ifndef FR_NO_UNROLL_NIB
       if constexpr (NIB && KS != KS_ANY) {
         // <= kNibbleMaxPrims primitives: the loop unrolled, so every index is an immediate
         // (the winner select needs no copy of the index into a VGPR) and the next record's
-        // scalar loads can be issued ahead
+        // scalar loads can be issued ahead. C3 trace 17.45 -> 17.29 ms (FR_NO_UNROLL_NIB: A/B)
 #pragma unroll
         for (uint32_t i = 0; i < kNibbleMaxPrims; ++i) {
           if (i >= sc.n) break;
