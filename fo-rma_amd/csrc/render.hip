@@ -955,10 +955,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       typedef std::integral_constant<uint32_t, FR_SPHERE> TagSphere;
 #ifndef FR_NO_UNROLL_NIB
       if constexpr (NIB && KS != KS_ANY) {
-        // <= kNibbleMaxPrims primitives: the loop unrolled, so every index is an immediate
-        // (the winner select needs no copy of the index into a VGPR) and the next record's
-        // scalar loads can be issued ahead. C3 trace 17.45 -> 17.29 ms (FR_NO_UNROLL_NIB: A/B)
-#pragma unroll
+        // <= kNibbleMaxPrims primitives: a counted loop over the compile-time bound with an
+        // early exit at n, whose record address advances by one add per primitive (the
+        // clang unroll of it does not happen for the box kernels; this form alone measured
+        // C3 trace 17.45 -> 17.29 ms; FR_NO_UNROLL_NIB keeps the plain loop for A/B)
         for (uint32_t i = 0; i < kNibbleMaxPrims; ++i) {
           if (i >= sc.n) break;
           if constexpr (KS == KS_AABB)
