@@ -712,7 +712,7 @@ def test_bvh_far_origins_from_stale_plane_records(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("depth", [8, 12, 50])
-def test_bvh_generator_10k_spheres_small(gpu, depth):
+def test_bvh_generator_10k_spheres_small(gpu, depth, monkeypatch):
     """C5's scene (tools/gen_scene.py --count 10000 --mesh sphere) at a size the oracle's
     brute-force loop finishes quickly; depth 12 and 50 run the u32-stack kernels."""
     import importlib.util
@@ -729,6 +729,11 @@ def test_bvh_generator_10k_spheres_small(gpu, depth):
     omean, ou8, ocnt, _ = O.render(prims, cam, w, h, spp, depth, threads=16)
     assert_parity(mean, u8, st, omean, ou8, ocnt)
     assert st["hits"] > 0
+    # the generator's spheres are all lambertian: the diffuse-only BVH kernels ran; the
+    # general shading step (FR_MAT=0) gives the same bits
+    monkeypatch.setenv("FR_MAT", "0")
+    mean0, u80, st0 = gpu.render(sc, sc.camera, w, h, spp, depth)
+    assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["segments"] == st["segments"]
 
 
 @pytest.mark.parametrize("scene,spp", [("scene_08", 3), ("scene_08", 37), ("random", 5)])
