@@ -980,26 +980,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       } else {
         // The list in order, as its kind runs: one scalar kind branch per run instead of a
         // dependent kind load and branch per primitive, and a tight loop per run whose
-        // record loads do not wait on a kind test (the same tests in the same order). The
-        // run bounds come from scalar loads, so the index is uniform without readfirstlane,
-        // and the record address advances by one add per primitive.
+        // record loads do not wait on a kind test (the same tests in the same order).
         typedef __attribute__((address_space(4))) const uint32_t cu32r;
         for (uint32_t rr = 0; rr < (list_walk ? sc.n_runs : 0u); ++rr) {
           const cu32r* rp = (cu32r*)(reinterpret_cast<uintptr_t>(sc.runs)) + 4u * __builtin_amdgcn_readfirstlane(rr);
           const uint32_t k = rp[0], i0 = rp[1], i1 = rp[2];
           if (k == FR_AABB) {
-            for (uint32_t i = i0; i < i1; ++i) test_one(TagAabb{}, i);
+            for (uint32_t i = i0; i < i1; ++i) test_one(TagAabb{}, __builtin_amdgcn_readfirstlane(i));
           } else if (k == FR_SPHERE) {
-            for (uint32_t i = i0; i < i1; ++i) test_one(TagSphere{}, i);
+            for (uint32_t i = i0; i < i1; ++i) test_one(TagSphere{}, __builtin_amdgcn_readfirstlane(i));
           } else if (k == FR_PLANE) {
             for (uint32_t i = i0; i < i1; ++i)
-              test_one(std::integral_constant<uint32_t, FR_PLANE>{}, i);
+              test_one(std::integral_constant<uint32_t, FR_PLANE>{}, __builtin_amdgcn_readfirstlane(i));
           } else if (k == FR_TRIANGLE) {
             for (uint32_t i = i0; i < i1; ++i)
-              test_one(std::integral_constant<uint32_t, FR_TRIANGLE>{}, i);
+              test_one(std::integral_constant<uint32_t, FR_TRIANGLE>{}, __builtin_amdgcn_readfirstlane(i));
           } else if (k == FR_OBB) {
             for (uint32_t i = i0; i < i1; ++i)
-              test_one(std::integral_constant<uint32_t, FR_OBB>{}, i);
+              test_one(std::integral_constant<uint32_t, FR_OBB>{}, __builtin_amdgcn_readfirstlane(i));
           }  // FR_STUB: never hits (aabb.rs:21-34, rectangle.rs:21-34)
         }
       }
