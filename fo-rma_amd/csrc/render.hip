@@ -1679,12 +1679,15 @@ static void launch_persistent(Kern kern, const Grid& g, size_t lds, hipStream_t 
     per_cu = 1;
   // the per-wave counter slots (fr_ctx::d_wcnt) hold kMaxWgPerCu workgroups per CU
   if (per_cu > static_cast<int>(kMaxWgPerCu)) per_cu = static_cast<int>(kMaxWgPerCu);
-  const char* no_stage = getenv("FR_BVH_STAGE");  // "0": BVH kernels store unstaged (A/B, tests)
-  if (g.stage_bytes && !(no_stage && strcmp(no_stage, "0") == 0)) {
+  // FR_BVH_STAGE: "0" BVH kernels store unstaged, "1" staged even at a lower residency (A/B, tests)
+  const char* stage_env = getenv("FR_BVH_STAGE");
+  const bool force_stage = stage_env && strcmp(stage_env, "1") == 0;
+  if (g.stage_bytes && !(stage_env && strcmp(stage_env, "0") == 0)) {
     int staged = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&staged, kern, static_cast<int>(kBlock), lds + g.stage_bytes) ==
             hipSuccess &&
-        staged >= per_cu) {
+        (staged >= per_cu || (force_stage && staged >= 1))) {
+      per_cu = staged < static_cast<int>(kMaxWgPerCu) ? staged : static_cast<int>(kMaxWgPerCu);
       lds += g.stage_bytes;
       a.kp.flags |= KF_STAGE;
     }
