@@ -423,6 +423,17 @@ __host__ __device__ __forceinline__ uint32_t stream_key(uint32_t bw) {
 // switch), else KS_ANY.
 enum { KS_ANY = 0, KS_AABB = 1, KS_SPHERE = 2 };
 
+// f(integral_constant<I>) for I = I0, I0 + 1, ... while I < n (n <= N), unrolled
+template <uint32_t I, uint32_t N, class F>
+__device__ __forceinline__ void unroll_below(uint32_t n, F& f) {
+  if constexpr (I < N) {
+    if (I < n) {
+      f(std::integral_constant<uint32_t, I>{});
+      unroll_below<I + 1u, N>(n, f);
+    }
+  }
+}
+
 // amdgpu_num_sgpr caps the scalar registers (MI355X_MICROARCH.md "Residency and
 // cooperative launch": <= 80 SGPRs admit 8 workgroups of 256 threads per CU, 82-96
 // admit 7). Measured on scene_08: 96 beats 80 (fewer SGPR spills) and 102.
@@ -798,6 +809,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                       static_cast<int>(recip_nr_ok(d.z));
       if (!rok) inv = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
       const float a_dd = dot(d, d);
+#ifndef FR_SPHERE_IEEE
+      const SphereSeg ssg = sphere_seg(a_dd);  // unused (removed) in kernels without spheres
+#endif
       float closest = FLT_MAX, t_last = 0.0f;
       int best = -1;
       // The node cull is conservative only for origins within kBvhOriginReach scene
@@ -903,7 +917,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               bool h = false;
               if (k == FR_SPHERE) {
                 const float4 g = r[0];
+#ifndef FR_SPHERE_IEEE
+                h = sphere_root_fast(xyz(g), g.w, o, d, a_dd, ssg, 0.001f, tmax, t);
+#else
                 h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, tmax, t);
+#endif
               } else if (k == FR_AABB) {
                 h = slab_root(slab3(xyz(r[0]), xyz(r[1]), o, inv), 0.001f, tmax, t);
               } else if (k == FR_TRIANGLE) {
@@ -933,7 +951,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           h = slab_root(slab3(xyz(r4[0]), xyz(r4[1]), o, inv), 0.001f, closest, t);
         } else if constexpr (K == FR_SPHERE) {
           const float4 g = r4[0];
+#ifndef FR_SPHERE_IEEE
+          h = sphere_root_fast(xyz(g), g.w, o, d, a_dd, ssg, 0.001f, closest, t);
+#else
           h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, closest, t);
+#endif
         } else if constexpr (K == FR_PLANE) {
           const int r = plane_test(xyz(r4[0]), xyz(r4[1]), xyz(r4[2]), o, d, 0.001f, closest, t);
           if (r) t_last = t;
@@ -955,17 +977,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       typedef std::integral_constant<uint32_t, FR_SPHERE> TagSphere;
 #ifndef FR_NO_UNROLL_NIB
       if constexpr (NIB && KS != KS_ANY) {
-        // <= kNibbleMaxPrims primitives: a counted loop over the compile-time bound with an
-        // early exit at n, whose record address advances by one add per primitive (the
-        // clang unroll of it does not happen for the box kernels; this form alone measured
-        // C3 trace 17.45 -> 17.29 ms; FR_NO_UNROLL_NIB keeps the plain loop for A/B)
-        for (uint32_t i = 0; i < kNibbleMaxPrims; ++i) {
-          if (i >= sc.n) break;
+        // <= kNibbleMaxPrims primitives: the tests unrolled over the compile-time bound with
+        // an exit at n, each index an inline constant (the winner select needs no index
+        // register) and each record at a constant offset. C3 trace 17.45 -> 17.29 ms as a
+        // counted loop with an exit, -> 16.95 ms unrolled; shard 0/8 -1.6 %
+        auto test_k = [&](auto ic) {
           if constexpr (KS == KS_AABB)
-            test_one(TagAabb{}, i);
+            test_one(TagAabb{}, decltype(ic)::value);
           else
-            test_one(TagSphere{}, i);
-        }
+            test_one(TagSphere{}, decltype(ic)::value);
+        };
+        // n through an empty asm here: otherwise the 15 tests' exit conditions are hoisted
+        // out of the lane loop as lane masks held (and spilled) in SGPRs
+        uint32_t n_here = sc.n;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+s"(n_here));
+#endif
+        unroll_below<0u, kNibbleMaxPrims>(n_here, test_k);
       } else
 #endif
       if constexpr (KS != KS_ANY) {
@@ -1394,6 +1422,23 @@ __global__ void ops_kernel(int op, const float* a, const float* b, uint32_t n, f
       break;
     }
     case 15: r = sky_t_fast(V3{x, y, b[(i + 1) % n]}); break;
+    case 16: {
+      // sphere_root_fast against sphere_root: thread 16k reads a[16k..16k+10] = centre,
+      // radius, origin, direction, t_max (t_min = 0.001). 0: same verdict and t bits;
+      // 1: verdicts differ; 2: both hit with different t
+      if (i % 16u != 0u || i + 16u > n) {
+        r = 0.0f;
+        break;
+      }
+      const float* q = a + i;
+      const V3 c{q[0], q[1], q[2]}, o{q[4], q[5], q[6]}, dv{q[7], q[8], q[9]};
+      const float aa = dot(dv, dv);
+      float t0 = 0.0f, t1 = 0.0f;
+      const bool h0 = sphere_root(c, q[3], o, dv, aa, 0.001f, q[10], t0);
+      const bool h1 = sphere_root_fast(c, q[3], o, dv, aa, sphere_seg(aa), 0.001f, q[10], t1);
+      r = h0 != h1 ? 1.0f : (h0 && __float_as_uint(t0) != __float_as_uint(t1)) ? 2.0f : 0.0f;
+      break;
+    }
     default: r = 0.0f;
   }
   out[i] = r;

@@ -265,6 +265,71 @@ __device__ __forceinline__ float div_rn(float a, float b, float y) {
 }
 #endif
 
+#if defined(__HIP__)
+// Correctly rounded sqrt(x) for x in [2^-96, 2^126]: v_sqrt_f32 and the compiler's two
+// FMA residual corrections, without its denormal scaling and class fix-up (identities in
+// that range; the same core as sky_t_fast, fr_selftest_ops op 14).
+__device__ __forceinline__ float sqrt_core(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sdn = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sup = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rdn = __builtin_fmaf(-sdn, s, x);
+  const float rup = __builtin_fmaf(-sup, s, x);
+  float r = rdn <= 0.0f ? sdn : s;
+  return rup > 0.0f ? sup : r;
+#else
+  return sqrtf(x);  // not used on the host
+#endif
+}
+
+// The segment's part of sphere_root_fast: ya = RN(1 / a) and whether a = dot(d, d) is in
+// [2^-60, 2^60] (recip_nr is exact there).
+struct SphereSeg {
+  float ya;
+  bool ok;
+};
+__device__ __forceinline__ SphereSeg sphere_seg(float a) {
+  return SphereSeg{recip_nr(a), (a >= 0x1p-60f) && (a <= 0x1p60f)};
+}
+
+// sphere_root bit for bit, with the root's sqrt and its two divisions by a done by their
+// core sequences (sqrt_core, div_rn with the segment's ya) on lanes where disc is in
+// [2^-96, 2^126], |b| <= 2^40 and a in [2^-60, 2^60]; other lanes take sphere_root's
+// expressions. There |-b -+ sq| <= 2^41 and a root that can be accepted (> t_min = 0.001)
+// has |numerator| >= 0.001 a >= 2^-70, so the numerator, the quotient (<= 2^101) and
+// every intermediate are normal and div_rn is the correctly rounded quotient; a root below
+// 0.001 in magnitude is below it by either sequence (a numerator under 2^-70 gives
+// |q| < 2^-10 with an absolute error far below the gap), so both reject it. Checked against
+// sphere_root on the device by fr_selftest_ops op 16 (tests/test_gpu_parity.py).
+__device__ __forceinline__ bool sphere_root_fast(V3 c, float radius, V3 o, V3 d, float a, SphereSeg sg,
+                                                 float t_min, float t_max, float& t) {
+  const V3 oc = sub(o, c);
+  const float b = dot(oc, d);
+  const float cc = dot(oc, oc) - radius * radius;
+  const float disc = b * b - a * cc;
+  if (disc > 0.0f) {
+    float r1, r2;
+    const bool fast = static_cast<int>(sg.ok) & static_cast<int>(disc >= 0x1p-96f) & static_cast<int>(disc <= 0x1p126f) &
+                      static_cast<int>(__builtin_fabsf(b) <= 0x1p40f);
+    if (fast) {
+      const float sq = sqrt_core(disc);
+      r1 = div_rn(-b - sq, a, sg.ya);
+      r2 = div_rn(-b + sq, a, sg.ya);
+    } else {
+      const float sq = sqrtf(disc);
+      r1 = (-b - sq) / a;
+      r2 = (-b + sq) / a;
+    }
+    const bool c1 = r1 > t_min && r1 < t_max;
+    const bool c2 = r2 > t_min && r2 < t_max;
+    t = c1 ? r1 : r2;
+    return c1 || c2;
+  }
+  return false;
+}
+#endif
+
 // maxNum(maxNum(a, b), c) in one v_max3_f32 (same IEEE-mode NaN rule as the chained
 // v_max_f32; device-checked against fmaxf chains in test_device_max3_matches_fmaxf).
 FR_HD float fmax3_num(float a, float b, float c) {

@@ -167,6 +167,67 @@ def test_fast_sky_parameter_is_bit_identical(gpu):
     assert not out.view(np.uint32).any(), int(np.count_nonzero(out.view(np.uint32)))
 
 
+def _sphere_cases(rng, m):
+    """Sphere-test inputs (centre, radius, origin, direction, t_max) of the kinds the kernel
+    meets and the fast root's guard edges; rows of 16 f32 (op 16's layout)."""
+    f32 = np.float32
+
+    def unit(v):
+        return v / np.linalg.norm(v, axis=0)
+
+    fams = []
+    # scatter rays: origin on the surface, direction n + a unit-ball point (lambertian)
+    c = rng.uniform(-20, 20, (3, m)); r = 10.0 ** rng.uniform(-2, 2, m); n = unit(rng.standard_normal((3, m)))
+    o = c + r * n; d = n + unit(rng.standard_normal((3, m))) * rng.uniform(0, 1, m) ** (1 / 3)
+    fams.append((c, r, o, d, np.where(rng.uniform(size=m) < 0.5, np.finfo(f32).max, rng.uniform(0.001, 100, m))))
+    # camera-like rays from anywhere at any scale
+    c = rng.uniform(-50, 50, (3, m)); r = 10.0 ** rng.uniform(-2, 2, m); o = rng.uniform(-10, 10, (3, m))
+    d = unit(c - o + rng.standard_normal((3, m)) * r) * 10.0 ** rng.uniform(-3, 1, m)
+    fams.append((c, r, o, d, np.full(m, np.finfo(f32).max)))
+    # every component of random sign and exponent (the guards' edges: a, b, disc ranges)
+    v = rng.standard_normal((11, m)) * 2.0 ** rng.uniform(-80, 80, (11, m))
+    fams.append((v[0:3], np.abs(v[3]), v[4:7], v[7:10], np.where(v[10] > 0, np.finfo(f32).max, np.abs(v[10]))))
+    # a and b across the guard bounds 2^-60 / 2^60 and 2^40
+    c = rng.uniform(-1, 1, (3, m)) * 2.0 ** rng.uniform(0, 45, m); r = np.abs(c[0]) * rng.uniform(0.1, 2, m)
+    o = rng.standard_normal((3, m)); d = unit(c - o + rng.standard_normal((3, m))) * 2.0 ** rng.uniform(-34, 34, m)
+    fams.append((c, r, o, d, np.full(m, np.finfo(f32).max)))
+    # grazing rays: disc near 0 (tiny and denormal discriminants)
+    c = rng.uniform(-20, 20, (3, m)); r = 10.0 ** rng.uniform(-2, 2, m); dh = unit(rng.standard_normal((3, m)))
+    pp = unit(np.cross(dh.T, rng.standard_normal((m, 3))).T)
+    o = c - 10 * r * dh + r * (1 + rng.uniform(-1e-6, 1e-6, m)) * pp
+    fams.append((c, r, o, dh * 10.0 ** rng.uniform(-2, 2, m), np.full(m, np.finfo(f32).max)))
+    # the near root at t ~ 0.001 (t_min) and the far root at t ~ t_max
+    c = rng.uniform(-20, 20, (3, m)); r = 10.0 ** rng.uniform(-1, 1, m); dh = unit(rng.standard_normal((3, m)))
+    s = 10.0 ** rng.uniform(-1, 1, m); o = c - dh * (r + 0.001 * s * rng.uniform(0.999, 1.001, m))
+    tfar = (2 * r + 0.001 * s) / s
+    fams.append((c, r, o, dh * s, tfar * rng.uniform(1 - 1e-6, 1 + 1e-6, m)))
+    rows = []
+    for c, r, o, d, tm in fams:
+        a = np.zeros((m, 16), dtype=f32)
+        a[:, 0:3] = c.T; a[:, 3] = r; a[:, 4:7] = o.T; a[:, 7:10] = d.T; a[:, 10] = tm
+        rows.append(a)
+    return np.concatenate(rows)
+
+
+def test_sphere_root_fast_is_bit_identical(gpu):
+    """The kernel's sphere test (rt_core.h sphere_root_fast: core sqrt and div_rn with the
+    segment's 1/a where the guards hold) against sphere_root's correctly rounded sqrt and
+    divisions (shapes/sphere.rs:23-51's arithmetic) on the device: same verdict and the same
+    t bits for every case (op 16)."""
+    import ctypes as C
+    rng = np.random.default_rng(16)
+    fp = C.POINTER(C.c_float)
+    for _ in range(4):
+        cases = _sphere_cases(rng, 100000).astype(np.float32)
+        x = np.ascontiguousarray(cases.reshape(-1))
+        out = np.empty_like(x)
+        gpu.check(gpu.lib().fr_selftest_ops(0, 16, x.ctypes.data_as(fp), x.ctypes.data_as(fp), x.size,
+                                            out.ctypes.data_as(fp)))
+        bad = out.reshape(-1, 16)[:, 0]
+        assert not bad.any(), (int(np.count_nonzero(bad == 1)), int(np.count_nonzero(bad == 2)),
+                               cases[np.nonzero(bad)[0][:3]].tolist())
+
+
 def test_device_schlick_unit_and_u8_match_oracle(gpu):
     import ctypes as C
     rng = np.random.default_rng(2)
