@@ -184,6 +184,11 @@ def _sphere_cases(rng, m):
     c = rng.uniform(-50, 50, (3, m)); r = 10.0 ** rng.uniform(-2, 2, m); o = rng.uniform(-10, 10, (3, m))
     d = unit(c - o + rng.standard_normal((3, m)) * r) * 10.0 ** rng.uniform(-3, 1, m)
     fams.append((c, r, o, d, np.full(m, np.finfo(f32).max)))
+    # rays leaving spheres they start outside of or near (the behind-the-origin skip)
+    c = rng.uniform(-50, 50, (3, m)); r = 10.0 ** rng.uniform(-2, 2, m)
+    o = c + unit(rng.standard_normal((3, m))) * r * rng.uniform(0.5, 1.5, m)
+    d = unit(o - c + rng.standard_normal((3, m)) * r * rng.uniform(0, 2, m)) * 10.0 ** rng.uniform(-3, 1, m)
+    fams.append((c, r, o, d, np.full(m, np.finfo(f32).max)))
     # every component of random sign and exponent (the guards' edges: a, b, disc ranges)
     v = rng.standard_normal((11, m)) * 2.0 ** rng.uniform(-80, 80, (11, m))
     fams.append((v[0:3], np.abs(v[3]), v[4:7], v[7:10], np.where(v[10] > 0, np.finfo(f32).max, np.abs(v[10]))))
