@@ -14,9 +14,13 @@
 
 #include <stdint.h>
 
+#if !defined(__HIPCC_RTC__)  // the constants below are also read by the run-time kernel build
 #include <vector>
 
 #include "../../include/forma_rt.h"
+#else
+#include "forma_rt.h"
+#endif
 
 namespace fr {
 
@@ -64,6 +68,7 @@ static_assert(sizeof(BvhSegment) == 16, "BvhSegment is one uint4");
 
 constexpr uint32_t kBvhMaxPlanes = 32;  // more planes: the in-order loop
 
+#if !defined(__HIPCC_RTC__)
 // Segments, nodes and the leaf-order primitive list (`order[slot]` = list index) for a
 // scene; false if the scene is too small, has too many planes or is too large for the
 // reference encoding. `force` drops the size and cost thresholds (A/B runs).
@@ -71,6 +76,7 @@ constexpr uint32_t kBvhMaxPlanes = 32;  // more planes: the in-order loop
 // boxes are padded by 1e-4 * (extent + 1).
 bool build_segments(const std::vector<fr_prim>& prims, std::vector<BvhSegment>& segs, std::vector<BvhNode>& nodes,
                     std::vector<uint32_t>& order, bool force = false, float* extent = nullptr);
+#endif
 
 // Ray origins the node cull is conservative for: |o| <= kBvhOriginReach * (extent + 1)
 // (the kernel's fused node slabs add |o| 2^-24 to a slab distance; the padding allows
@@ -82,8 +88,10 @@ constexpr float kBvhOriginReach = 100.0f;
 // slab >= 1e-4 * 2^100 ~ 1e26 wide, and |o| 2^100 stays finite.
 constexpr float kBvhInvClamp = 0x1p100f;
 
+#if !defined(__HIPCC_RTC__)
 // Largest internal-node depth of the trees (root = 0): below kBvhStack by construction.
 uint32_t bvh_max_depth(const std::vector<BvhSegment>& segs, const std::vector<BvhNode>& nodes);
+#endif
 
 }  // namespace fr
 

@@ -21,7 +21,9 @@
 #pragma once
 #include <stdint.h>
 
-#if defined(__HIPCC__) || defined(__HIP__)
+#if defined(__HIPCC_RTC__)
+#define FR_HD __host__ __device__ __forceinline__  // hiprtc (trace_kernel.h's run-time build)
+#elif defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define FR_HD __host__ __device__ __forceinline__
 #else

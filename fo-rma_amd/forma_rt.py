@@ -27,12 +27,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FORMA_RT_LIB") or os.path.join(HERE, "libforma_rt.so")
 SCENES_DIR = os.path.join(HERE, "scenes")
 
-FR_ABI_VERSION = 4  # include/forma_rt.h FR_ABI_VERSION
+FR_ABI_VERSION = 5  # include/forma_rt.h FR_ABI_VERSION
 FR_OK, FR_EARG, FR_EPARSE, FR_EHIP, FR_ENODEV, FR_ENOMEM = 0, -1, -2, -3, -4, -5
 FR_SPHERE, FR_PLANE, FR_AABB, FR_OBB, FR_STUB, FR_TRIANGLE = 0, 1, 2, 3, 4, 5
 FR_LAMBERTIAN, FR_METAL, FR_DIELECTRIC, FR_LIGHT = 0, 1, 2, 3
 FR_FLAG_WRITE_U8 = 1
 FR_FLAG_MT_BANDS = 2  # save_image_mt semantics (forma_rt.h)
+FR_FLAG_SCENE_JIT = 4  # scene-specialised trace kernel (hiprtc, cached; same image bits)
 MAX_DEPTH = 50  # tracer.rs:10
 DEFAULT_SEED = 0x5EED
 
@@ -86,7 +87,8 @@ EXPORTS = (
     "fr_ctx_trace_log_read", "fr_mctx_create", "fr_mctx_free", "fr_mctx_count", "fr_mctx_ctx", "fr_mctx_render",
     "fr_mctx_sync", "fr_mctx_frame", "fr_mctx_download",
     "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_recip",
-    "fr_post_process", "fr_post_process_device", "fr_rgb_to_rgba_device",
+    "fr_post_process", "fr_post_process_device", "fr_rgb_to_rgba_device", "fr_ctx_jit_info", "fr_selftest_jit",
+    "fr_ctx_prepare",
 )
 
 _lib = None
@@ -170,6 +172,10 @@ def lib():
         L.fr_rgb_to_rgba_device.argtypes = [vp, vp, vp, C.c_size_t]
     if hasattr(L, "fr_selftest_recip"):  # absent from A/B builds of older sources
         L.fr_selftest_recip.argtypes = [C.c_int, C.c_uint64, C.c_uint64, P(C.c_uint64), P(C.c_uint32)]
+    if hasattr(L, "fr_ctx_jit_info"):  # absent from A/B builds of older sources
+        L.fr_ctx_jit_info.argtypes = [vp, P(C.c_int), P(C.c_double), P(C.c_int)]
+        L.fr_ctx_prepare.argtypes = [vp, vp, P(FrCamera), P(FrParams)]
+        L.fr_selftest_jit.argtypes = [C.c_char_p, P(C.c_uint32), C.c_uint32, P(C.c_int), P(C.c_size_t), P(C.c_double)]
     _lib = L
     return L
 
@@ -391,11 +397,12 @@ def scene_path(name):
 # ---- rendering ----------------------------------------------------------------
 
 def make_params(width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, shard_index=0, shard_count=1,
-                write_u8=True, mt_bands=False):
+                write_u8=True, mt_bands=False, scene_jit=False):
     p = FrParams()
     p.width, p.height, p.spp, p.max_depth, p.seed = width, height, spp, max_depth, seed
     p.strip_rows, p.shard_index, p.shard_count = 8, shard_index, shard_count
-    p.flags = (FR_FLAG_WRITE_U8 if write_u8 else 0) | (FR_FLAG_MT_BANDS if mt_bands else 0)
+    p.flags = ((FR_FLAG_WRITE_U8 if write_u8 else 0) | (FR_FLAG_MT_BANDS if mt_bands else 0) |
+               (FR_FLAG_SCENE_JIT if scene_jit else 0))
     return p
 
 
@@ -488,6 +495,19 @@ class RenderContext:
     def wait(self):
         """Block until every render and download enqueued on this context has finished."""
         check(lib().fr_ctx_wait(self._h))
+
+    def prepare(self, scene, cam, params):
+        """Set up everything a render of `params` needs (scene copy, buffers, and with
+        scene_jit the scene-specialised kernel) without rendering; returns jit_info()."""
+        check(lib().fr_ctx_prepare(self._h, scene._h, C.byref(cam), C.byref(params)))
+        return self.jit_info()
+
+    def jit_info(self):
+        """The last render's trace kernel: {"used": scene-specialised kernel ran, "ms": time
+        that render spent getting it (compile or cache load), "compiled": hiprtc ran}."""
+        used, ms, comp = C.c_int(0), C.c_double(0.0), C.c_int(0)
+        check(lib().fr_ctx_jit_info(self._h, C.byref(used), C.byref(ms), C.byref(comp)))
+        return {"used": bool(used.value), "ms": ms.value, "compiled": bool(comp.value)}
 
     def trace_log(self, enable=True):
         """Start (or stop) logging every trace-kernel launch's HIP-event duration."""
@@ -582,14 +602,16 @@ class MultiContext:
 
 
 def render(scene, cam, width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, device=0, shard_index=0,
-           shard_count=1, n_gpus=1, mt_bands=False):
+           shard_count=1, n_gpus=1, mt_bands=False, scene_jit=False):
     """Render on the GPU. Returns (mean[H,W,3] f32, u8[H,W,3], stats). Rows outside the
     shard are NaN / 0. n_gpus > 1 row-shards the whole image across devices 0..n-1.
-    mt_bands: save_image_mt semantics (mean then holds the u8 average, 0..255)."""
+    mt_bands: save_image_mt semantics (mean then holds the u8 average, 0..255).
+    scene_jit: the scene-specialised trace kernel (FR_FLAG_SCENE_JIT; same bits)."""
     mean = np.full((height, width, 3), np.nan, dtype=np.float32)
     u8 = np.zeros((height, width, 3), dtype=np.uint8)
     st = FrStats()
-    p = make_params(width, height, spp, max_depth, seed, shard_index, shard_count, mt_bands=mt_bands)
+    p = make_params(width, height, spp, max_depth, seed, shard_index, shard_count, mt_bands=mt_bands,
+                    scene_jit=scene_jit)
     fm, fu = mean.ctypes.data_as(C.POINTER(C.c_float)), u8.ctypes.data_as(C.POINTER(C.c_uint8))
     if n_gpus > 1:
         check(lib().fr_render_hip_multi(scene._h, C.byref(cam), C.byref(p), n_gpus, fm, fu, C.byref(st)))

@@ -40,18 +40,21 @@
 #ifndef FORMA_RT_H
 #define FORMA_RT_H
 
+#if !defined(__HIPCC_RTC__) /* hiprtc (the scene-specialised build) provides these types */
 #include <stddef.h>
+#endif
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define FR_ABI_VERSION 4 /* 2: fr_stats.trace_launches; FR_TRIANGLE; post effects; FR_FLAG_MT_BANDS
+#define FR_ABI_VERSION 5 /* 2: fr_stats.trace_launches; FR_TRIANGLE; post effects; FR_FLAG_MT_BANDS
                             3: fr_stats.scatters/.occupancy; fr_ctx_download_async, fr_ctx_wait,
                                fr_host_alloc/free; item-major sample buffer
                             4: fr_mctx_* (persistent multi-device context); fr_ctx_trace_log(_read);
-                               entry points restore the caller's current HIP device */
+                               entry points restore the caller's current HIP device
+                            5: FR_FLAG_SCENE_JIT, fr_ctx_prepare, fr_ctx_jit_info */
 
 /* error codes */
 #define FR_OK 0
@@ -83,6 +86,13 @@ extern "C" {
    holds acc (0..255). Render the plain simple scene (fr_scene_builtin 0) with
    max_depth 50 to match the reference call. */
 #define FR_FLAG_MT_BANDS 2u
+/* Scene-specialised trace kernel (render.hip / jit.cpp): for list-loop scenes of at most 64
+   primitives, compile the kernel once per scene with the primitive records as constants
+   (hiprtc; cached per process and on disk, FR_JIT_CACHE). Same image bits as without the
+   flag; shared slab planes are computed once per segment. The first render of a scene
+   pays the compile (seconds; fr_ctx_jit_info reports it). FR_SCENE_JIT=1 / 0 in the
+   environment forces it on / off for every render. */
+#define FR_FLAG_SCENE_JIT 4u
 
 /*
  * One primitive, in the order it is tested (list order decides ties, tracer.rs:195-200).
@@ -208,6 +218,15 @@ int fr_ctx_device_buffers(fr_ctx* ctx, float** d_mean_rgb, uint8_t** d_rgb8);
    entries logged. Lets a caller streaming K frames average all K of them. */
 int fr_ctx_trace_log(fr_ctx* ctx, int enable);
 int fr_ctx_trace_log_read(fr_ctx* ctx, int which, double* ms, uint32_t cap, uint32_t* n);
+/* Everything a render of these parameters sets up before its first launch, without
+   rendering: the scene's device copy, the output and sample buffers and, with
+   FR_FLAG_SCENE_JIT, the scene-specialised kernel (compiled or loaded here, so the first
+   timed frame does not pay for it). fr_ctx_jit_info then describes that kernel. */
+int fr_ctx_prepare(fr_ctx* ctx, fr_scene* scene, const fr_camera* cam, const fr_params* params);
+/* The last render's trace kernel: *used = 1 when it ran the scene-specialised kernel
+   (FR_FLAG_SCENE_JIT), *ms = the time that render spent getting it (hiprtc compile, disk
+   cache load or 0 when already loaded), *compiled = 1 when hiprtc ran. Any may be NULL. */
+int fr_ctx_jit_info(fr_ctx* ctx, int* used, double* ms, int* compiled);
 
 /* ---- persistent multi-device context (tracer.rs:83-134 render_mt, one device per shard) ----
    Entry i of `devices` renders row shard i of n of every frame on its own fr_ctx (device
@@ -277,6 +296,12 @@ int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, 
    1.0f / x for every f32 bit pattern in [base, base + count): mismatches per exponent
    field in bad[256], first mismatching pattern in first[256] (0xFFFFFFFF = none). */
 int fr_selftest_recip(int device, uint64_t base, uint64_t count, uint64_t* bad, uint32_t* first);
+/* No device needed: hiprtc compiles the scene-specialised kernel for `arch` with n 64-B
+   device records (16 u32 each, kind in word 15); targs = trace_kernel's 8 template
+   arguments, or NULL for the headline's (all boxes, diffuse, depth <= 8, 8-B records);
+   *code_bytes = the code object's size, *ms = the compile time. */
+int fr_selftest_jit(const char* arch, const uint32_t* rec, uint32_t n, const int* targs, size_t* code_bytes,
+                    double* ms);
 
 #ifdef __cplusplus
 }

@@ -16,12 +16,12 @@ if [ "$rev" = "." ]; then
 else
   git -C "$root" archive "$rev" fo-rma_amd/csrc include | tar -x -C "$tmp"
 fi
-make -C "$root/fo-rma_amd" -s build/scene.o build/json_min.o build/bvh.o build/post.o
+make -C "$root/fo-rma_amd" -s build/scene.o build/json_min.o build/bvh.o build/post.o build/jit.o
 mkdir -p "$root/fo-rma_amd/build/ab"
 FP="-ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP -fno-slp-vectorize $defs \
   -c "$tmp/fo-rma_amd/csrc/render.hip" -o "$tmp/render.o"
 b="$root/fo-rma_amd/build"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$b/ab/libforma_rt_$name.so" "$tmp/render.o" \
-  "$b/scene.o" "$b/json_min.o" "$b/bvh.o" "$b/post.o"
+  "$b/scene.o" "$b/json_min.o" "$b/bvh.o" "$b/post.o" "$b/jit.o" -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 echo "$b/ab/libforma_rt_$name.so"
