@@ -540,7 +540,16 @@ struct fr_ctx {
   int occupancy = 0;  // trace-kernel workgroups per CU of the last launch (occupancy API)
   float* d_mean = nullptr;
   uint8_t* d_u8 = nullptr;
-  unsigned long long* d_cnt = nullptr;  // [0..3] counters, [4..] diagnostics; [31] queue head
+  // [0..3] counters, [4..] diagnostics; [31] queue head: one set of 32 per frame slot
+  unsigned long long* d_cnt = nullptr;
+  unsigned long long* last_cnt = nullptr;  // the last render's set
+  // Frame pipeline (FR_FRAME_PIPE): one-pass frames alternate between two
+  // frame slots (sample buffer half, counter set), so frame k+1's trace starts when frame k's
+  // trace ends while frame k's sum runs beside it; ev_fslot[s] = the end of the last sum
+  // that used slot s, which the next frame on that slot waits for.
+  int frame_slot = 0;
+  hipEvent_t ev_fslot[2] = {nullptr, nullptr};
+  bool fslot_used[2] = {false, false};
   unsigned long long* d_wcnt = nullptr;  // per-wave partial counters (KWork::wave_counters)
   uint32_t wcnt_waves = 0;               // their capacity in waves
   float* d_samples = nullptr;
@@ -595,6 +604,7 @@ struct Grid {
   int* per_cu;    // out: resident workgroups per CU
   uint32_t* blocks;  // out: workgroups launched
   size_t stage_bytes;  // BVH kernels: LDS for sample staging, taken if it costs no residency
+  uint32_t reserve = 0;  // workgroup slots per CU left free (frame pipeline: the previous frame's sum)
 };
 
 // The scene-specialised kernel request of one render (jit.h): on for list-loop launches
@@ -680,6 +690,7 @@ static int launch_persistent(const Grid& g, size_t lds, hipStream_t st, KArgs a,
       a.kp.flags |= KF_STAGE;
     }
   }
+  if (g.reserve && per_cu > static_cast<int>(g.reserve)) per_cu -= static_cast<int>(g.reserve);
   *g.per_cu = per_cu;
   uint64_t cap = static_cast<uint64_t>(per_cu) * static_cast<uint64_t>(g.num_cus);
   // FR_MAX_WGS=k caps the grid (tests: with a few workgroups every wave claims many
@@ -812,7 +823,9 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
       hipStreamCreateWithFlags(&c->stream_sum, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream_copy, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming) != hipSuccess ||
-      hipMalloc(&c->d_cnt, 32 * sizeof(unsigned long long)) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fslot[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fslot[1], hipEventDisableTiming) != hipSuccess ||
+      hipMalloc(&c->d_cnt, 2 * 32 * sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&c->d_wcnt, 2 * 3 * sizeof(unsigned long long) * kMaxWgPerCu * (kBlock / 64u) * c->num_cus) !=
           hipSuccess) {  // one set per pass slot (traces of consecutive passes overlap)
     fr_ctx_free(c);
@@ -832,6 +845,8 @@ void fr_ctx_free(fr_ctx* c) {
     if (s) (void)hipStreamSynchronize(s);
   if (c->stream_copy) (void)hipStreamSynchronize(c->stream_copy), (void)hipStreamDestroy(c->stream_copy);
   if (c->ev_copy) (void)hipEventDestroy(c->ev_copy);
+  for (hipEvent_t e : c->ev_fslot)
+    if (e) (void)hipEventDestroy(e);
   if (c->d_mean) (void)hipFree(c->d_mean);
   if (c->d_u8) (void)hipFree(c->d_u8);
   if (c->d_cnt) (void)hipFree(c->d_cnt);
@@ -982,7 +997,14 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       nb_pass = static_cast<uint32_t>(cap_blocks / 2);  // two slots must fit
   }
   const int passes = nb_pass ? static_cast<int>((nblocks + nb_pass - 1) / nb_pass) : 0;
-  const int slots = passes > 1 ? 2 : 1;
+  // frame pipeline (fr_ctx::frame_slot): one-pass frames whose sample buffer fits twice
+  // (FR_FRAME_PIPE=0 turns it off). Streamed scene_08 frames, shard 0 of N on one MI355X:
+  // 17.01 -> 16.59 ms at N = 1, 2.52 -> 2.29 ms at N = 8
+  const char* fp_env = getenv("FR_FRAME_PIPE");
+  const bool fpipe = passes == 1 && !(fp_env && strcmp(fp_env, "0") == 0) && cap_blocks >= 2u * nblocks;
+  const int fs = fpipe ? c->frame_slot : 0;
+  unsigned long long* cnt = c->d_cnt + 32 * fs;
+  const int slots = passes > 1 || fpipe ? 2 : 1;
   const size_t slot_bytes = per_block * nb_pass;
   if (kp.P && nb_pass && slot_bytes * slots > c->cap_samples) {
     if (c->d_samples) HIPCHK(hipFree(c->d_samples));
@@ -1035,7 +1057,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     jr.on = want && build_ok && !use_bvh && dc->n >= 1 && dc->n <= kJitMaxPrims;
   }
   KWork kw;
-  kw.counters = c->d_cnt;
+  kw.counters = cnt;
   if (dry) {
     jr.dry = true;
     if (jr.on && kp.P) {
@@ -1051,7 +1073,9 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     return FR_OK;
   }
   c->t0 = std::chrono::steady_clock::now();
-  HIPCHK(hipMemsetAsync(c->d_cnt, 0, 32 * sizeof(unsigned long long), c->stream));
+  // the last frame that used this slot's counters and samples has been summed
+  if (c->fslot_used[fs]) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_fslot[fs], 0));
+  HIPCHK(hipMemsetAsync(cnt, 0, 32 * sizeof(unsigned long long), c->stream));
 #ifdef FR_DIAG
   {
     const unsigned long long z[2] = {0, 0};
@@ -1071,7 +1095,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   int traced = 0;  // trace launches whose events were recorded
   int summed = 0;
   for (int pass = 0; pass < passes || (pass == 0 && kp.P); ++pass) {
-    const int slot = pass % 2;
+    const int slot = fpipe ? fs : pass % 2;
     hipStream_t ts = slot ? c->stream2 : c->stream;
     float* samples = c->d_samples ? c->d_samples + static_cast<size_t>(slot) * (slot_bytes / sizeof(float)) : nullptr;
     kp.b0 = static_cast<uint32_t>(pass) * nb_pass;
@@ -1088,12 +1112,17 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     }
     if (kp.n_items) {
       if (pass >= 2) HIPCHK(hipStreamWaitEvent(ts, c->ev_sum[pass - 2], 0));  // the slot's last reader is done
-      kw.queue = reinterpret_cast<uint32_t*>(c->d_cnt + 31 - slot);
+      kw.queue = reinterpret_cast<uint32_t*>(cnt + 31 - (fpipe ? 0 : slot));
       kw.samples = samples;
       // persistent grid: the resident workgroup count (launch_persistent)
       uint32_t blocks = 0;
-      const Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy, &blocks,
-                      use_bvh && stage_n > 1 ? kBlock * stage_n * 3 * sizeof(float) : 0u};
+      Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy, &blocks,
+                use_bvh && stage_n > 1 ? kBlock * stage_n * 3 * sizeof(float) : 0u};
+      // pipelined frames leave room on every CU for the previous frame's sum workgroups
+      if (fpipe) {
+        const char* r = getenv("FR_FRAME_PIPE_RESERVE");
+        grid.reserve = r ? static_cast<uint32_t>(atoi(r)) : 1u;
+      }
       unsigned long long* wcnt = c->d_wcnt + static_cast<size_t>(slot) * 3 * kMaxWgPerCu * (kBlock / 64u) * c->num_cus;
       kw.wave_counters = wcnt;
       HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), ts));
@@ -1109,7 +1138,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       // the sums, so fr_ctx_sync reads d_cnt after every pass's reduce, and the next
       // frame's d_cnt memset (c->stream) cannot overtake a reduce of this one
       hipLaunchKernelGGL(reduce_counters, dim3(1), dim3(256), 0, c->stream_sum, wcnt, blocks * (kBlock / 64u),
-                         c->d_cnt);
+                         cnt);
       HIPCHK(hipGetLastError());
       ++traced;
     }
@@ -1123,12 +1152,22 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     summed = pass + 1;
     if (last) break;
   }
-  if (summed) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_sum[summed - 1], 0));
+  // frame end: on the context's stream (the next frame's trace waits for this one's sums),
+  // or, pipelined, on the sum stream (the next frame's trace starts when this trace ends)
+  hipStream_t end_stream = c->stream;
+  if (fpipe)
+    end_stream = c->stream_sum;
+  else if (summed)
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_sum[summed - 1], 0));
+  HIPCHK(hipEventRecord(c->ev_fslot[fs], end_stream));
+  c->fslot_used[fs] = true;
+  c->last_cnt = cnt;
+  if (fpipe) c->frame_slot ^= 1;
   c->passes = traced;
   c->jit_used = jr.used;
   c->jit_stats = jr.stats;
-  HIPCHK(hipEventRecord(c->ev1, c->stream));
-  if (c->log_on) HIPCHK(log_end(c, 1, c->stream));
+  HIPCHK(hipEventRecord(c->ev1, end_stream));
+  if (c->log_on) HIPCHK(log_end(c, 1, end_stream));
   c->last = *p;
   c->last_n = dc->n;
   c->pending = true;
@@ -1140,9 +1179,10 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
   SET_DEVICE(c->device);
   HIPCHK(hipStreamSynchronize(c->stream));
   if (!c->pending) return set_error(FR_EARG, "fr_ctx_sync: nothing rendered");
+  HIPCHK(hipEventSynchronize(c->ev1));  // the frame's end (on the sum stream when pipelined)
   if (st) {
     unsigned long long cnt[32] = {};
-    HIPCHK(hipMemcpy(cnt, c->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cnt, c->last_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
 #ifdef FR_PROF
     {
       double tot = 0;
@@ -1273,6 +1313,7 @@ static int enqueue_download(fr_ctx* c, hipStream_t st, float* mean_rgb, uint8_t*
 int fr_ctx_download(fr_ctx* c, float* mean_rgb, uint8_t* rgb8) {
   if (!c || !c->pending) return set_error(FR_EARG, "fr_ctx_download: nothing rendered");
   SET_DEVICE(c->device);
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev1, 0));  // the last render's end (its sums)
   const int rc = enqueue_download(c, c->stream, mean_rgb, rgb8);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(c->stream));

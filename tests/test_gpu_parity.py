@@ -521,12 +521,14 @@ def test_context_reuse_and_scene_edits(gpu):
     ctx.close()
 
 
-@pytest.mark.parametrize("shard", [(0, 1), (1, 3)])
-def test_streamed_frames_match_the_oracle(gpu, shard):
+@pytest.mark.parametrize("shard,pipe", [((0, 1), "0"), ((1, 3), "0"), ((0, 1), "1"), ((1, 3), "1")])
+def test_streamed_frames_match_the_oracle(gpu, shard, pipe, monkeypatch):
     """bench.py's loop: frames enqueued back to back on one context, each followed by its
     asynchronous gather into the same pinned host frame, one sync after the last. The
     streams alone order the frames, so the host frame holds the last frame's strips
-    exactly, and the counters are that frame's."""
+    exactly, and the counters are that frame's. pipe "1": the frame pipeline (FR_FRAME_PIPE,
+    frame k+1's trace beside frame k's sum)."""
+    monkeypatch.setenv("FR_FRAME_PIPE", pipe)
     w, h, spp, depth = 64, 40, 20, 8
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
     prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path("scene_08")).read())
@@ -544,6 +546,32 @@ def test_streamed_frames_match_the_oracle(gpu, shard):
     ctx.wait()
     assert_parity(frame.mean.copy(), frame.u8.copy(), st, omean, ou8, ocnt, rows=rows)
     frame.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("jit", [False, True])
+def test_pipelined_frames_of_different_seeds(gpu, jit, monkeypatch):
+    """Five frames of different seeds enqueued back to back with the frame pipeline, each
+    gathered into its own pinned frame: every gather holds its own frame (the two frame
+    slots are reused every other frame), equal to the frame rendered alone."""
+    w, h, spp, depth = 64, 40, 33, 8
+    sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
+    seeds = [3, 4, 5, 6, 7]
+    refs = [gpu.render(sc, sc.camera, w, h, spp, depth, seed=sd) for sd in seeds]
+    monkeypatch.setenv("FR_FRAME_PIPE", "1")
+    ctx = gpu.RenderContext(0)
+    frames = [gpu.PinnedFrame(w, h) for _ in seeds]
+    for sd, fr_ in zip(seeds, frames):
+        ctx.render(sc, sc.camera, gpu.make_params(w, h, spp, depth, seed=sd, scene_jit=jit))
+        ctx.download_async(fr_)
+    st = ctx.sync()
+    ctx.wait()
+    for (m, u, _), fr_ in zip(refs, frames):
+        assert np.array_equal(fr_.mean.view(np.uint32), m.view(np.uint32)) and np.array_equal(fr_.u8, u)
+    assert (st["segments"], st["hits"], st["scatters"]) == (refs[-1][2]["segments"], refs[-1][2]["hits"],
+                                                            refs[-1][2]["scatters"])
+    for fr_ in frames:
+        fr_.close()
     ctx.close()
 
 
