@@ -666,18 +666,21 @@ def test_c3_headline_frame_in_full(gpu):
     """C3, the config the headline number is quoted on (scene_08 at 1920x1080, 256 spp, 8
     bounces; tracer.rs:160-187's whole image), through the HIP path and the oracle: all
     2,073,600 pixels (530.8 M samples) compared — means within 1e-5 and bit for bit, u8
-    identical — and the whole-frame segment, hit and scatter counters equal."""
+    identical — and the whole-frame segment, hit and scatter counters equal. Both trace
+    kernels: the compiled-in one and the scene-specialised one bench.py runs (DESIGN.md
+    §4.11)."""
     name, w, h, spp, depth = "scene_08", 1920, 1080, 256, 8
     sc = gpu.Scene.from_file(gpu.scene_path(name), w, h)
-    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
-    assert st["samples"] == w * h * spp == 530841600
+    runs = [gpu.render(sc, sc.camera, w, h, spp, depth, scene_jit=jit) for jit in (False, True)]
+    assert runs[0][2]["samples"] == w * h * spp == 530841600
     prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path(name)).read())
     cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
     omean, ou8, ocnt = O.render_rows(prims, cam, w, h, spp, depth, range(h), threads=oracle_threads(), chunk=120,
                                      progress=_progress("C3"))
-    assert ocnt["samples"] == st["samples"]
-    assert_parity(mean, u8, st, omean, ou8, ocnt)
-    assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
+    for mean, u8, st in runs:
+        assert ocnt["samples"] == st["samples"]
+        assert_parity(mean, u8, st, omean, ou8, ocnt)
+        assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
 
 
 @pytest.mark.slow
@@ -688,6 +691,10 @@ def test_c2_on_row_subset(gpu):
     sc = gpu.Scene.from_file(gpu.scene_path(name), w, h)
     mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
     assert st["samples"] == w * h * spp
+    # the scene-specialised kernel renders the same frame bit for bit
+    jm, ju, jst = gpu.render(sc, sc.camera, w, h, spp, depth, scene_jit=True)
+    assert np.array_equal(jm.view(np.uint32), mean.view(np.uint32)) and np.array_equal(ju, u8)
+    assert (jst["segments"], jst["hits"], jst["scatters"]) == (st["segments"], st["hits"], st["scatters"])
     prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path(name)).read())
     cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
     omean, ou8, ocnt, n = O.render(prims, cam, w, h, spp, depth, row_step=step, threads=oracle_threads())
