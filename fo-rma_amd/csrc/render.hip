@@ -127,6 +127,14 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
                                                           const float4* __restrict__ att, uint32_t n_prims) {
   constexpr uint32_t kSumSlot = WPS * kBlockSamples + 1;  // floats per slot in LDS (odd stride)
   __shared__ float tile[kSumThreads * kSumSlot];
+#ifndef FR_SUM_PRIO
+#define FR_SUM_PRIO 3
+#endif
+  // Pipelined frames run this kernel on the CU slot the next frame's
+  // trace leaves free; at the trace waves' priority its four waves got about an eighth of
+  // the CU's issue and took as long as the trace. Raised, they take their few
+  // instructions' issue slots first and the sum keeps pace with its memory traffic.
+  if (FR_SUM_PRIO) __builtin_amdgcn_s_setprio(FR_SUM_PRIO);
   __shared__ float att_s[3 * (kDeferUnit + 1)];  // KF_DEFER: attenuation rgb, entry kDeferUnit = 1
   const uint32_t t = threadIdx.x;
   const bool defer = (kp.flags & KF_DEFER) != 0;
@@ -547,9 +555,12 @@ struct fr_ctx {
   // frame slots (sample buffer half, counter set), so frame k+1's trace starts when frame k's
   // trace ends while frame k's sum runs beside it; ev_fslot[s] = the end of the last sum
   // that used slot s, which the next frame on that slot waits for.
-  int frame_slot = 0;
-  hipEvent_t ev_fslot[2] = {nullptr, nullptr};
-  bool fslot_used[2] = {false, false};
+  static constexpr int kFrameSlots = 3;
+  int frame_slot = 0, frame_parity = 0;
+  int fs_n = 0;            // slots in the current layout (2 or 3; 0: not pipelined)
+  size_t fs_bytes = 0;     // sample-buffer bytes per slot in that layout
+  hipEvent_t ev_fslot[kFrameSlots] = {nullptr, nullptr, nullptr};
+  bool fslot_used[kFrameSlots] = {false, false, false};
   unsigned long long* d_wcnt = nullptr;  // per-wave partial counters (KWork::wave_counters)
   uint32_t wcnt_waves = 0;               // their capacity in waves
   float* d_samples = nullptr;
@@ -825,8 +836,10 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
       hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fslot[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fslot[1], hipEventDisableTiming) != hipSuccess ||
-      hipMalloc(&c->d_cnt, 2 * 32 * sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc(&c->d_wcnt, 2 * 3 * sizeof(unsigned long long) * kMaxWgPerCu * (kBlock / 64u) * c->num_cus) !=
+      hipEventCreateWithFlags(&c->ev_fslot[2], hipEventDisableTiming) != hipSuccess ||
+      hipMalloc(&c->d_cnt, fr_ctx::kFrameSlots * 32 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&c->d_wcnt, fr_ctx::kFrameSlots * 3 * sizeof(unsigned long long) * kMaxWgPerCu * (kBlock / 64u) *
+                                c->num_cus) !=
           hipSuccess) {  // one set per pass slot (traces of consecutive passes overlap)
     fr_ctx_free(c);
     return set_error(FR_EHIP, "fr_ctx_create: event/counter allocation failed");
@@ -1000,12 +1013,31 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   // frame pipeline (fr_ctx::frame_slot): one-pass frames whose sample buffer fits twice
   // (FR_FRAME_PIPE=0 turns it off). Streamed scene_08 frames, shard 0 of N on one MI355X:
   // 17.01 -> 16.59 ms at N = 1, 2.52 -> 2.29 ms at N = 8
+  // Traces: frame k+1's trace follows frame k's on one stream, or, for a shard with fewer
+  // pixel slots than the grid has lanes (one item per lane and block: the queue's drain is a
+  // large part of the frame, e.g. shard 0 of 8), the two slots' traces run on two streams,
+  // so the next frame's trace fills the CUs the previous one's drain leaves idle: shard 0/8
+  // 2.47 -> 2.31 ms per frame, the same at N <= 4. FR_FRAME_PIPE=1 / 2
+  // forces serial / overlapping traces.
+  // Three slots when the budget holds them (a sum beside a trace runs about as long as the
+  // trace, so frame k + 2 would otherwise wait for frame k's sum), else two.
   const char* fp_env = getenv("FR_FRAME_PIPE");
-  const bool fpipe = passes == 1 && !(fp_env && strcmp(fp_env, "0") == 0) && cap_blocks >= 2u * nblocks;
-  const int fs = fpipe ? c->frame_slot : 0;
-  unsigned long long* cnt = c->d_cnt + 32 * fs;
-  const int slots = passes > 1 || fpipe ? 2 : 1;
+  const int nfs = passes != 1 || (fp_env && strcmp(fp_env, "0") == 0) ? 0
+                  : cap_blocks >= 3u * nblocks                        ? 3
+                  : cap_blocks >= 2u * nblocks                        ? 2
+                                                                      : 0;
+  const bool fpipe = nfs > 0;
+  const uint64_t grid_lanes = static_cast<uint64_t>(c->num_cus) * (kMaxWgPerCu - 1u) * kBlock;
+  const bool fpipe_overlap =
+      fpipe && (fp_env && *fp_env ? strcmp(fp_env, "2") == 0 : static_cast<uint64_t>(kp.P) < grid_lanes);
   const size_t slot_bytes = per_block * nb_pass;
+  // a new layout (slot count or size, or not pipelined): every earlier frame must have been
+  // summed before this one reuses the buffers; in one layout only this slot's last user
+  const bool relayout = !fpipe || nfs != c->fs_n || slot_bytes != c->fs_bytes;
+  if (relayout) c->frame_slot = 0;
+  const int fs = fpipe ? c->frame_slot % nfs : 0;
+  unsigned long long* cnt = c->d_cnt + 32 * fs;
+  const int slots = passes > 1 ? 2 : fpipe ? nfs : 1;
   if (kp.P && nb_pass && slot_bytes * slots > c->cap_samples) {
     if (c->d_samples) HIPCHK(hipFree(c->d_samples));
     c->d_samples = nullptr;
@@ -1073,8 +1105,12 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     return FR_OK;
   }
   c->t0 = std::chrono::steady_clock::now();
-  // the last frame that used this slot's counters and samples has been summed
-  if (c->fslot_used[fs]) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_fslot[fs], 0));
+  // the last frame that used this slot's counters and samples (or, after a layout change,
+  // every earlier frame) has been summed
+  for (int k = 0; k < fr_ctx::kFrameSlots; ++k)
+    if (c->fslot_used[k] && (k == fs || relayout)) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_fslot[k], 0));
+  c->fs_n = nfs;
+  c->fs_bytes = slot_bytes;
   HIPCHK(hipMemsetAsync(cnt, 0, 32 * sizeof(unsigned long long), c->stream));
 #ifdef FR_DIAG
   {
@@ -1096,7 +1132,8 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   int summed = 0;
   for (int pass = 0; pass < passes || (pass == 0 && kp.P); ++pass) {
     const int slot = fpipe ? fs : pass % 2;
-    hipStream_t ts = slot ? c->stream2 : c->stream;
+    // one trace stream for pipelined frames: frame k+1's trace follows frame k's trace
+    hipStream_t ts = fpipe ? (fpipe_overlap && c->frame_parity ? c->stream2 : c->stream) : slot ? c->stream2 : c->stream;
     float* samples = c->d_samples ? c->d_samples + static_cast<size_t>(slot) * (slot_bytes / sizeof(float)) : nullptr;
     kp.b0 = static_cast<uint32_t>(pass) * nb_pass;
     kp.nb = pass < passes ? min(nb_pass, nblocks - kp.b0) : 0u;
@@ -1162,7 +1199,10 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   HIPCHK(hipEventRecord(c->ev_fslot[fs], end_stream));
   c->fslot_used[fs] = true;
   c->last_cnt = cnt;
-  if (fpipe) c->frame_slot ^= 1;
+  if (fpipe) {
+    c->frame_slot = (fs + 1) % nfs;
+    c->frame_parity ^= 1;
+  }
   c->passes = traced;
   c->jit_used = jr.used;
   c->jit_stats = jr.stats;

@@ -521,13 +521,15 @@ def test_context_reuse_and_scene_edits(gpu):
     ctx.close()
 
 
-@pytest.mark.parametrize("shard,pipe", [((0, 1), "0"), ((1, 3), "0"), ((0, 1), "1"), ((1, 3), "1")])
+@pytest.mark.parametrize("shard,pipe", [((0, 1), "0"), ((1, 3), "0"), ((0, 1), "1"), ((1, 3), "1"), ((0, 1), "2"),
+                                        ((1, 3), "2"), ((0, 1), ""), ((1, 3), "")])
 def test_streamed_frames_match_the_oracle(gpu, shard, pipe, monkeypatch):
     """bench.py's loop: frames enqueued back to back on one context, each followed by its
     asynchronous gather into the same pinned host frame, one sync after the last. The
     streams alone order the frames, so the host frame holds the last frame's strips
     exactly, and the counters are that frame's. pipe "1": the frame pipeline (FR_FRAME_PIPE,
-    frame k+1's trace beside frame k's sum)."""
+    frame k+1's trace beside frame k's sum); "2": consecutive traces may overlap too; "":
+    the default choice."""
     monkeypatch.setenv("FR_FRAME_PIPE", pipe)
     w, h, spp, depth = 64, 40, 20, 8
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
@@ -549,8 +551,8 @@ def test_streamed_frames_match_the_oracle(gpu, shard, pipe, monkeypatch):
     ctx.close()
 
 
-@pytest.mark.parametrize("jit", [False, True])
-def test_pipelined_frames_of_different_seeds(gpu, jit, monkeypatch):
+@pytest.mark.parametrize("jit,pipe", [(False, "1"), (True, "1"), (False, "2"), (True, "2")])
+def test_pipelined_frames_of_different_seeds(gpu, jit, pipe, monkeypatch):
     """Five frames of different seeds enqueued back to back with the frame pipeline, each
     gathered into its own pinned frame: every gather holds its own frame (the two frame
     slots are reused every other frame), equal to the frame rendered alone."""
@@ -558,7 +560,7 @@ def test_pipelined_frames_of_different_seeds(gpu, jit, monkeypatch):
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
     seeds = [3, 4, 5, 6, 7]
     refs = [gpu.render(sc, sc.camera, w, h, spp, depth, seed=sd) for sd in seeds]
-    monkeypatch.setenv("FR_FRAME_PIPE", "1")
+    monkeypatch.setenv("FR_FRAME_PIPE", pipe)
     ctx = gpu.RenderContext(0)
     frames = [gpu.PinnedFrame(w, h) for _ in seeds]
     for sd, fr_ in zip(seeds, frames):

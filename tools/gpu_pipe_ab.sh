@@ -4,8 +4,8 @@ mkdir -p gpurun_out/pipe_ab
 export FR_JIT_CACHE=$PWD/gpurun_out/pipe_ab/jitcache
 for rep in 1 2; do
   for n in 1 2 4 8; do
-    FR_FRAME_PIPE=0 timeout -k 10 120 python -u tools/shard_stream.py $n 30 || exit 1
-    FR_FRAME_PIPE=1 timeout -k 10 120 python -u tools/shard_stream.py $n 30 || exit 1
-    FR_FRAME_PIPE=1 FR_FRAME_PIPE_RESERVE=0 timeout -k 10 120 python -u tools/shard_stream.py $n 30 || exit 1
+    for pipe in 0 1 2; do
+      FR_FRAME_PIPE=$pipe timeout -k 10 120 python -u tools/shard_stream.py $n 30 || exit 1
+    done
   done
 done
