@@ -398,8 +398,11 @@ def run_steps(ctx, scene, cam, params, frame, steps, sync_each=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    # 20 frames (0.35 s of GPU time at N = 1): the frame pipeline's steady state, in which a
+    # frame's sum runs beside the next frame's trace; the first and last
+    # frames' sums are inside the timed region too
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes")
     ap.add_argument("--cpu-budget", type=float, default=12.0)

@@ -128,12 +128,12 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   constexpr uint32_t kSumSlot = WPS * kBlockSamples + 1;  // floats per slot in LDS (odd stride)
   __shared__ float tile[kSumThreads * kSumSlot];
 #ifndef FR_SUM_PRIO
-#define FR_SUM_PRIO 3
+#define FR_SUM_PRIO 0
 #endif
   // Pipelined frames run this kernel on the CU slot the next frame's
-  // trace leaves free; at the trace waves' priority its four waves got about an eighth of
-  // the CU's issue and took as long as the trace. Raised, they take their few
-  // instructions' issue slots first and the sum keeps pace with its memory traffic.
+  // trace leaves free, where it takes about as long as the trace. A raised wave priority
+  // (FR_SUM_PRIO=3) made it keep pace but slowed the trace by 4 % (C3 streamed 16.65 ->
+  // 17.07 ms per frame): not used.
   if (FR_SUM_PRIO) __builtin_amdgcn_s_setprio(FR_SUM_PRIO);
   __shared__ float att_s[3 * (kDeferUnit + 1)];  // KF_DEFER: attenuation rgb, entry kDeferUnit = 1
   const uint32_t t = threadIdx.x;
