@@ -701,7 +701,9 @@ static int launch_persistent(const Grid& g, size_t lds, hipStream_t st, KArgs a,
       a.kp.flags |= KF_STAGE;
     }
   }
-  if (g.reserve && per_cu > static_cast<int>(g.reserve)) per_cu -= static_cast<int>(g.reserve);
+  // only full 8-workgroup grids give a slot up: the BVH kernels (6 per CU) lost a sixth of
+  // their grid for a sum of a twentieth of their frame (C5 55.6 -> 58.0 ms)
+  if (g.reserve && per_cu >= static_cast<int>(kMaxWgPerCu)) per_cu -= static_cast<int>(g.reserve);
   *g.per_cu = per_cu;
   uint64_t cap = static_cast<uint64_t>(per_cu) * static_cast<uint64_t>(g.num_cus);
   // FR_MAX_WGS=k caps the grid (tests: with a few workgroups every wave claims many
