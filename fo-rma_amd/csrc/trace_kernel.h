@@ -60,8 +60,11 @@ constexpr uint32_t kMaxWgPerCu = 8;   // 2048 threads per CU / kBlock: the persi
 // ... for the 8-B-record kernels (scenes of <= 15 primitives, the headline's): measured
 // C3 trace 20.81 -> 20.69 ms at 6 (7 and 8 the same within noise); 6 on the other kernels
 // cost C2 +1.7 % and a 10k-sphere BVH frame +1.2 %, so they keep FR_KREJ
+// Re-tuned for the scene-specialised kernel (round 3): 9 with
+// FR_CLAIM_MIN_NIB 3 streams C3 at 16.49 ms per frame against 16.63 (6 / 2), three runs;
+// shard 0/8 unchanged (tools/gpu_knob_shards.sh, profiles/r03k_knob_shards.log)
 #ifndef FR_KREJ_NIB
-#define FR_KREJ_NIB 6
+#define FR_KREJ_NIB 9
 #endif
 #ifndef FR_CLAIM_MIN
 #define FR_CLAIM_MIN 1  // lanes that must wait for an item before the wave claims (tuning only)
@@ -69,7 +72,7 @@ constexpr uint32_t kMaxWgPerCu = 8;   // 2048 threads per CU / kBlock: the persi
 // ... for the 8-B-record kernels (the headline's): C3 18.50 -> 18.28 ms at 2 (18.31 at 4, 18.46
 // at 6); 4 on every kernel cost C2 +2 %, so the others keep FR_CLAIM_MIN
 #ifndef FR_CLAIM_MIN_NIB
-#define FR_CLAIM_MIN_NIB 2
+#define FR_CLAIM_MIN_NIB 3
 #endif
 #ifndef FR_NUM_SGPR
 #define FR_NUM_SGPR 96
