@@ -1092,18 +1092,23 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   }
   KWork kw;
   kw.counters = cnt;
+  // the scene-specialised kernel is compiled or loaded here, before anything is enqueued,
+  // so a first frame's events do not span the compile
+  JitStats jit_got{};
+  if (jr.on && kp.P) {
+    JitReq pre = jr;
+    pre.dry = true;
+    uint32_t blocks = 0;
+    int occ = 0;
+    const Grid grid{1, c->num_cus, &occ, &blocks, 0};
+    rc = launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, grid, lds, c->stream, KArgs{ks, kc, kp, kw},
+                      &pre);
+    if (rc) return rc;
+    jit_got = pre.stats;
+  }
   if (dry) {
-    jr.dry = true;
-    if (jr.on && kp.P) {
-      uint32_t blocks = 0;
-      int occ = 0;
-      const Grid grid{1, c->num_cus, &occ, &blocks, 0};
-      rc = launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, grid, lds, c->stream, KArgs{ks, kc, kp, kw},
-                        &jr);
-      if (rc) return rc;
-    }
-    c->jit_used = jr.used;
-    c->jit_stats = jr.stats;
+    c->jit_used = jr.on && kp.P;
+    c->jit_stats = jit_got;
     return FR_OK;
   }
   c->t0 = std::chrono::steady_clock::now();
@@ -1207,7 +1212,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   }
   c->passes = traced;
   c->jit_used = jr.used;
-  c->jit_stats = jr.stats;
+  c->jit_stats = jit_got;
   HIPCHK(hipEventRecord(c->ev1, end_stream));
   if (c->log_on) HIPCHK(log_end(c, 1, end_stream));
   c->last = *p;
