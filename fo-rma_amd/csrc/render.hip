@@ -126,7 +126,12 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
                                                           uint8_t* __restrict__ out_u8, int first, int last,
                                                           const float4* __restrict__ att, uint32_t n_prims) {
   constexpr uint32_t kSumSlot = WPS * kBlockSamples + 1;  // floats per slot in LDS (odd stride)
-  __shared__ float tile[kSumThreads * kSumSlot];
+  // one LDS block, the attenuation table first: its entries then sit at LDS byte offset
+  // 12 x index, and the per-level reads need no base-address add (the table behind the
+  // tile, at 33,792 B, cost a v_or per level: 8 of ~60 VALU per sample)
+  __shared__ float lds_sum[3 * (kDeferUnit + 1) + kSumThreads * kSumSlot];
+  float* const att_s = lds_sum;  // KF_DEFER: attenuation rgb, entry kDeferUnit = 1
+  float* const tile = lds_sum + 3 * (kDeferUnit + 1);
 #ifndef FR_SUM_PRIO
 #define FR_SUM_PRIO 0
 #endif
@@ -135,7 +140,6 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   // (FR_SUM_PRIO=3) made it keep pace but slowed the trace by 4 % (C3 streamed 16.65 ->
   // 17.07 ms per frame): not used.
   if (FR_SUM_PRIO) __builtin_amdgcn_s_setprio(FR_SUM_PRIO);
-  __shared__ float att_s[3 * (kDeferUnit + 1)];  // KF_DEFER: attenuation rgb, entry kDeferUnit = 1
   const uint32_t t = threadIdx.x;
   const bool defer = (kp.flags & KF_DEFER) != 0;
   if (defer) {  // kSumThreads == kDeferUnit + 1
