@@ -342,7 +342,15 @@ class Barrier:
             import torch.distributed as dist
             self.dist = dist
             if not dist.is_initialized():
-                dist.init_process_group("gloo")
+                # gloo's connection message goes to fd 1: keep stdout for the one JSON line
+                sys.stdout.flush()
+                saved = os.dup(1)
+                os.dup2(2, 1)
+                try:
+                    dist.init_process_group("gloo")
+                finally:
+                    os.dup2(saved, 1)
+                    os.close(saved)
 
     def __call__(self):
         if self.world > 1:
