@@ -1020,11 +1020,12 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   // (FR_FRAME_PIPE=0 turns it off). Streamed scene_08 frames, shard 0 of N on one MI355X:
   // 17.01 -> 16.59 ms at N = 1, 2.52 -> 2.29 ms at N = 8
   // Traces: frame k+1's trace follows frame k's on one stream, or, for a shard with fewer
-  // pixel slots than the grid has lanes (one item per lane and block: the queue's drain is a
-  // large part of the frame, e.g. shard 0 of 8), the two slots' traces run on two streams,
-  // so the next frame's trace fills the CUs the previous one's drain leaves idle: shard 0/8
-  // 2.47 -> 2.31 ms per frame, the same at N <= 4. FR_FRAME_PIPE=1 / 2
-  // forces serial / overlapping traces.
+  // than two pixel slots per grid lane (two items per lane and block or fewer: the queue's
+  // drain is a large part of the frame, shards 0 of 4 and of 8), consecutive frames' traces
+  // alternate between two streams, so the next frame's trace fills the CUs the previous
+  // one's drain leaves idle: shard 0/8 2.47 -> 2.29 ms per frame, 0/4 4.27-4.46 -> 4.28
+  // (steadier), the same at N = 1 and 2, where serial traces keep each launch's own event
+  // time. FR_FRAME_PIPE=1 / 2 forces serial / overlapping traces.
   // Three slots when the budget holds them (a sum beside a trace runs about as long as the
   // trace, so frame k + 2 would otherwise wait for frame k's sum), else two.
   const char* fp_env = getenv("FR_FRAME_PIPE");
@@ -1035,7 +1036,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   const bool fpipe = nfs > 0;
   const uint64_t grid_lanes = static_cast<uint64_t>(c->num_cus) * (kMaxWgPerCu - 1u) * kBlock;
   const bool fpipe_overlap =
-      fpipe && (fp_env && *fp_env ? strcmp(fp_env, "2") == 0 : static_cast<uint64_t>(kp.P) < grid_lanes);
+      fpipe && (fp_env && *fp_env ? strcmp(fp_env, "2") == 0 : static_cast<uint64_t>(kp.P) < 2u * grid_lanes);
   const size_t slot_bytes = per_block * nb_pass;
   // a new layout (slot count or size, or not pipelined): every earlier frame must have been
   // summed before this one reuses the buffers; in one layout only this slot's last user
