@@ -205,11 +205,23 @@ int jit_compile_probe(const char* arch, const JitSpec& spec, size_t* code_bytes,
   return FR_OK;
 }
 
+// The device's target name (gcnArchName), queried once per device: every render of a
+// scene-specialised frame looks its kernel up, and the property query is not free.
+static std::string device_arch(int device) {
+  static std::mutex mu;
+  static std::map<int, std::string> arch;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = arch.find(device);
+  if (it != arch.end()) return it->second;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return "";
+  return arch[device] = prop.gcnArchName;
+}
+
 int jit_trace_kernel(int device, const JitSpec& spec, hipFunction_t* out, JitStats* stats) {
   const auto t0 = std::chrono::steady_clock::now();
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return set_error(FR_EHIP, "hipGetDeviceProperties failed");
-  const std::string arch = prop.gcnArchName;
+  const std::string arch = device_arch(device);
+  if (arch.empty()) return set_error(FR_EHIP, "hipGetDeviceProperties failed");
   const std::string prelude = make_prelude(spec);
   const char* xo = getenv("FR_JIT_OPTS");
   const std::string key = hex_key(std::string(jit_src::kHash) + "\n" + arch + "\n" + spec.name_expr + "\n" + prelude +
