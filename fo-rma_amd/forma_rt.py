@@ -663,11 +663,12 @@ class TraceModel:
             self.ctx = RenderContext(self.device)
         return self.ctx
 
-    def render(self, scene, spp, max_depth, seed, mt_bands=False):
-        """One frame on the model's context: (mean[H,W,3], u8[H,W,3], stats)."""
+    def render(self, scene, spp, max_depth, seed, mt_bands=False, scene_jit=False):
+        """One frame on the model's context: (mean[H,W,3], u8[H,W,3], stats). scene_jit: the
+        trace kernel compiled for the scene (same bits; worth it for many-sample renders)."""
         ctx = self.context()
         ctx.render(scene, self.scene.camera, make_params(self.width, self.height, spp, max_depth, seed,
-                                                         mt_bands=mt_bands))
+                                                         mt_bands=mt_bands, scene_jit=scene_jit))
         self.last_stats = ctx.sync()
         mean, u8 = ctx.download(self.width, self.height)
         return mean, u8, self.last_stats
@@ -738,7 +739,7 @@ def save_image_mt(model, sample, path="out/basic_mt.png", max_depth=MAX_DEPTH):
     scene, scenes::get_simple_scene, with the model's camera), each pass gamma-corrected
     to u8, the u8 frames averaged and truncated, PNG."""
     simple = Scene.builtin(0, model.width, model.height)
-    acc, u8, stats = model.render(simple, sample, max_depth, model.seed, mt_bands=True)
+    acc, u8, stats = model.render(simple, sample, max_depth, model.seed, mt_bands=True, scene_jit=True)
     write_png(path, u8)
     return acc, u8, stats
 
@@ -746,6 +747,6 @@ def save_image_mt(model, sample, path="out/basic_mt.png", max_depth=MAX_DEPTH):
 def save_image(model, sample, path="out/basic.png", max_depth=MAX_DEPTH):
     """tracer.rs:160-187: `sample` spp per pixel, gamma 2, u8, PNG. Like the reference it
     fails if the output directory is missing (tracer.rs:186 unwrap)."""
-    mean, u8, stats = model.render(model.scene, sample, max_depth, model.seed)
+    mean, u8, stats = model.render(model.scene, sample, max_depth, model.seed, scene_jit=True)
     write_png(path, u8)
     return mean, u8, stats
