@@ -382,17 +382,18 @@ def test_multi_device_api_with_one_device(gpu):
     assert np.array_equal(a, b) and np.array_equal(au, bu)
 
 
-@pytest.mark.parametrize("n", [2, 8])
-def test_multi_context_matches_one_device_bit_for_bit(gpu, n):
+@pytest.mark.parametrize("n,jit", [(2, False), (8, False), (2, True), (8, True)])
+def test_multi_context_matches_one_device_bit_for_bit(gpu, n, jit):
     """fr_mctx (tracer.rs:83-134's row tiling, one context per shard) with every entry on
     device 0: the stitched frame equals the N = 1 render bit for bit, frame after frame, and
     the contexts' device buffers and the page-locked host frame stay the same across
-    frames (nothing is allocated per frame)."""
+    frames (nothing is allocated per frame). jit: every context runs the scene-specialised
+    kernel (one module per device, shared by its contexts)."""
     w, h, spp, depth = 100, 70, 20, 8  # H % 8 != 0: the last strip is partial
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
     ref, ref_u8, ref_st = gpu.render(sc, sc.camera, w, h, spp, depth)
     m = gpu.MultiContext([0] * n)
-    p = gpu.make_params(w, h, spp, depth)
+    p = gpu.make_params(w, h, spp, depth, scene_jit=jit)
     bufs, hostp = None, None
     for _ in range(3):
         m.render(sc, sc.camera, p)
