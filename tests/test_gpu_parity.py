@@ -957,10 +957,13 @@ def test_absorbed_paths_skip_unwind_only_when_exact(gpu, colors):
     assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
 
 
-@pytest.mark.parametrize("pipe,buf_gb", [("1", None), ("2", None), ("3", None), ("5", None), ("2", "0.0002")])
-def test_pass_pipeline_never_changes_results(gpu, pipe, buf_gb, monkeypatch):
+@pytest.mark.parametrize("pipe,buf_gb,jit", [("1", None, False), ("2", None, False), ("3", None, False),
+                                            ("5", None, False), ("2", "0.0002", False), ("3", None, True),
+                                            ("2", "0.0002", True)])
+def test_pass_pipeline_never_changes_results(gpu, pipe, buf_gb, jit, monkeypatch):
     """Passes on alternating streams with a double-buffered sample buffer (and, with a
-    tiny FR_SAMPLE_BUFFER_GB, many passes reusing the two slots) give the same bits."""
+    tiny FR_SAMPLE_BUFFER_GB, many passes reusing the two slots) give the same bits; jit:
+    the passes run the scene-specialised kernel."""
     w, h, spp = 64, 40, 70  # 5 blocks, the last partial
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
     monkeypatch.setenv("FR_PIPELINE", "1")
@@ -969,7 +972,7 @@ def test_pass_pipeline_never_changes_results(gpu, pipe, buf_gb, monkeypatch):
     monkeypatch.setenv("FR_PIPELINE", pipe)
     if buf_gb:
         monkeypatch.setenv("FR_SAMPLE_BUFFER_GB", buf_gb)
-    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, 8)
+    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, 8, scene_jit=jit)
     assert np.array_equal(mean.view(np.uint32), ref[0].view(np.uint32)) and np.array_equal(u8, ref[1])
     assert (st["segments"], st["hits"]) == (ref[2]["segments"], ref[2]["hits"])
 
