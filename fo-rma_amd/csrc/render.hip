@@ -129,9 +129,12 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   // one LDS block, the attenuation table first: its entries then sit at LDS byte offset
   // 12 x index, and the per-level reads need no base-address add (the table behind the
   // tile, at 33,792 B, cost a v_or per level: 8 of ~60 VALU per sample)
-  __shared__ float lds_sum[3 * (kDeferUnit + 1) + kSumThreads * kSumSlot];
-  float* const att_s = lds_sum;  // KF_DEFER: attenuation rgb, entry kDeferUnit = 1
-  float* const tile = lds_sum + 3 * (kDeferUnit + 1);
+  // 8-B records (WPS 2) read a 16-B-stride copy of the first 16 entries: level k's byte
+  // offset is then one shift-and-mask of the winners word (below)
+  __shared__ float lds_sum[4 * 16 + 3 * (kDeferUnit + 1) + kSumThreads * kSumSlot];
+  float4* const att16 = reinterpret_cast<float4*>(lds_sum);
+  float* const att_s = lds_sum + 4 * 16;  // KF_DEFER: attenuation rgb, entry kDeferUnit = 1
+  float* const tile = att_s + 3 * (kDeferUnit + 1);
 #ifndef FR_SUM_PRIO
 #define FR_SUM_PRIO 0
 #endif
@@ -147,6 +150,7 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
     att_s[3 * t] = a.x;
     att_s[3 * t + 1] = a.y;
     att_s[3 * t + 2] = a.z;
+    if (t < 16u) att16[t] = make_float4(a.x, a.y, a.z, 0.0f);
   }
   const uint32_t q0 = blockIdx.x * kSumThreads, q = q0 + t;
   const uint32_t nq = min(kSumThreads, kp.P - q0);
@@ -202,10 +206,14 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
           // 8-B record: terminal, then a_7 ... a_0 from 4-bit entries (kNibbleUnit: 1)
           const uint32_t tb = __float_as_uint(c[0]), w = __float_as_uint(c[1]);
           V3 col = tb == kDeferAbsorbed ? V3{0.0f, 0.0f, 0.0f} : sky_from_t(c[0]);
+          // level k's entry at byte 16 x nibble k: odd levels are the high nibble of byte
+          // k / 2 of w, even levels the high nibble of byte k / 2 of w << 4
+          const uint32_t w4 = w << 4;
 #pragma unroll
           for (int k = 7; k >= 0; --k) {
-            const float* e = att_s + 3u * ((w >> (4 * k)) & 0xFu);
-            col = mul(V3{e[0], e[1], e[2]}, col);
+            const uint32_t off = (((k & 1) ? w : w4) >> (8 * (k >> 1))) & 0xF0u;
+            const float4 e = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(att16) + off);
+            col = mul(V3{e.x, e.y, e.z}, col);
           }
           sum = add(sum, col);
         } else if (defer) {
