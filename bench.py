@@ -4,8 +4,14 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+    FR_BENCH_DEVICES=0,0 python bench.py --gpus 2     (rehearsal: two shards on device 0)
 
-One process per GPU. A step renders the whole frame and gathers it to the host: rank r
+Two ways to run N > 1 (launch_plan): a plain `python bench.py --gpus N` drives devices
+0..N-1 from this one process through fr_mctx, the drop-in's multi-device context
+(tracer.rs:83-134's row tiling with a device per band; run_mctx), and reports every
+shard's trace time beside the wall time of the whole frames; under torch.distributed.run
+each rank is one process per GPU (run_rank). The frames and their stitched image are the
+same either way. Per rank: a step renders the rank's strips and gathers them to the host: rank r
 renders the 8-row strips k with k % N == r (no collective on the data path) and copies
 its strips (f32 means and the u8 image) into page-locked host memory, the "final gather
 to host" (BASELINE.md §4). The gather of frame k runs on its own stream while frame k+1
@@ -57,11 +63,43 @@ N_SIMDS = 1024             # 256 CUs x 4 SIMDs; a wave64 VALU instruction issues
 FLOPS_H = os.path.join(ROOT, "fo-rma_amd", "csrc", "flops.h")
 
 
-def dist_env():
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+def dist_env(env=None):
+    env = os.environ if env is None else env
+    rank = int(env.get("RANK", "0"))
+    world = int(env.get("WORLD_SIZE", "1"))
+    local = int(env.get("LOCAL_RANK", str(rank)))
     return rank, world, local
+
+
+def launch_plan(gpus, env=None):
+    """How this process runs `gpus` GPUs. Returns {"mode", "rank", "world", "devices"}:
+    - "ranks": launched by torch.distributed.run (WORLD_SIZE > 1), one process per GPU;
+      this rank renders shard RANK of WORLD_SIZE on device LOCAL_RANK (FR_BENCH_DEVICE
+      overrides it: every rank on one device, a rehearsal);
+    - "mctx": a plain `python bench.py --gpus N` (N > 1): this one process drives fr_mctx
+      over devices 0..N-1, shard i on device i — the drop-in's own multi-device path
+      (tracer.rs:83-134's row tiling, one device per band); FR_BENCH_DEVICES=0,0,...
+      (N entries) lists the devices instead, so one GPU rehearses an N-shard run;
+    - "single": N = 1 (FR_BENCH_DEVICES=d picks the device).
+    Raises SystemExit on an inconsistent request."""
+    env = os.environ if env is None else env
+    rank, world, local = dist_env(env)
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    if world > 1:
+        if gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} under a launcher with WORLD_SIZE={world}")
+        dev = int(env["FR_BENCH_DEVICE"]) if env.get("FR_BENCH_DEVICE") not in (None, "") else local
+        return {"mode": "ranks", "rank": rank, "world": world, "devices": [dev]}
+    spec = env.get("FR_BENCH_DEVICES", "")
+    if spec.strip():
+        devices = [int(x) for x in spec.split(",") if x.strip()]
+        if len(devices) != gpus or min(devices) < 0:
+            raise SystemExit(f"bench.py: FR_BENCH_DEVICES={spec!r} must list {gpus} device ids")
+    else:
+        dev = int(env["FR_BENCH_DEVICE"]) if gpus == 1 and env.get("FR_BENCH_DEVICE") not in (None, "") else 0
+        devices = [dev] if gpus == 1 else list(range(gpus))
+    return {"mode": "mctx" if gpus > 1 else "single", "rank": 0, "world": 1, "devices": devices}
 
 
 def shard_rows(height, shard, shards, strip=8):
@@ -403,45 +441,178 @@ def run_steps(ctx, scene, cam, params, frame, steps, sync_each=False):
     return [ctx.sync()] * steps if steps else []
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    # 20 frames (0.35 s of GPU time at N = 1): the frame pipeline's steady state, in which a
-    # frame's sum runs beside the next frame's trace (DESIGN.md §4.5b); the first and last
-    # frames' sums are inside the timed region too
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--verify", action="store_true", help="stitch the frame on rank 0 and report a checksum")
-    ap.add_argument("--sync-each", action="store_true", help="wait for each frame's stats before the next")
-    ap.add_argument("--no-scene-jit", action="store_true",
-                    help="run the compiled-in trace kernel instead of the scene-specialised one (same image)")
-    a = ap.parse_args()
 
-    rank, world, local = dist_env()
-    # rehearsal only: run every rank on one device (timing is then meaningless)
-    if os.environ.get("FR_BENCH_DEVICE") is not None:
-        local = int(os.environ["FR_BENCH_DEVICE"])
-    if world == 1 and a.gpus > 1:
-        sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    import torch
-
-    import forma_rt as fr  # after torch, so one HIP runtime serves both
-
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local)
-    barrier = Barrier(world)
-    scene = fr.Scene.from_file(fr.scene_path(SCENE), WIDTH, HEIGHT)
-    cam = scene.camera
-    n_prims = len(scene)
+def scene_kinds(fr, scene):
+    """Primitive count per kind name (flops.h's kFlopTest<Kind> names)."""
     kinds = {}
     for p in scene.prims():
         name = {fr.FR_SPHERE: "Sphere", fr.FR_PLANE: "Plane", fr.FR_AABB: "Box", fr.FR_OBB: "Obb",
                 fr.FR_TRIANGLE: "Triangle"}.get(p.kind)
         if name:
             kinds[name] = kinds.get(name, 0) + 1
+    return kinds
+
+
+def rooflines(counts, kinds, pixels, n_prims, launches, launch_ms, traffic=None, issue=None):
+    """The trace kernel's rooflines per launch on one device: FP32 VALU (the binding bound)
+    and HBM (the north star's ask), from the algorithmic work of `counts` over `launches`
+    launches of `launch_ms` each."""
+    c = flop_constants()
+    flops_launch = algorithmic_flops(c, counts, kinds, pixels) / launches
+    tflops = flops_launch / (launch_ms * 1e-3) / 1e12
+    bytes_launch = algorithmic_bytes(pixels, n_prims) / launches
+    gbs = bytes_launch / (launch_ms * 1e-3) / 1e9
+    roof = {"bound": "valu", "achieved": round(tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / FP32_PEAK_TFLOPS, 5), "traffic": round(traffic) if traffic else None,
+            "peak_no_fma": NO_FMA_PEAK_TOPS, "frac_no_fma": round(tflops / NO_FMA_PEAK_TOPS, 5),
+            "peak_no_fma_rule": "1024 SIMDs x 32 lanes/clk x 2.4 GHz (no contraction: 1 op per lane-slot)",
+            "kernel": "trace_kernel", "flops_per_launch": round(flops_launch),
+            "flop_model": "fo-rma_amd/csrc/flops.h x exact counters", "valu_issue": issue}
+    hbm = {"bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 8), "bytes_per_launch": round(bytes_launch),
+           "traffic": round(traffic) if traffic else None,
+           "measured_gbs": round(traffic / (launch_ms * 1e-3) / 1e9, 2) if traffic else None}
+    return roof, hbm
+
+
+def base_line(a, n_gpus, value, elapsed, parallelism):
+    return {
+        "metric": "Msamples/sec (pixels×spp) at 1920×1080, 256 spp, 8 bounces; 1/2/4/8 GPU",
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": n_gpus,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "reference scene file scenes/scene_08.json (bundled), fixed RNG seed 0x5EED",
+        "config": {"workload": f"{SCENE} {WIDTH}x{HEIGHT} {SPP}spp {DEPTH} bounces (BASELINE config 3)",
+                   "scene": SCENE, "width": WIDTH, "height": HEIGHT, "spp": SPP, "max_depth": DEPTH, "seed": SEED,
+                   "parallelism": parallelism},
+    }
+
+
+def frame_hash(mean):
+    import hashlib
+    return hashlib.sha256(mean.tobytes()).hexdigest()[:16]
+
+
+def run_mctx(a, plan, torch, fr):
+    """N > 1 in one process: fr_mctx over plan["devices"], shard i of N on entry i, every
+    frame's strips gathered asynchronously into the context's page-locked host frame.
+    A step = one whole frame on all devices (enqueued back to back, no host wait between
+    frames); the timed region ends when every device's last gather has landed, so the wall
+    time is the slowest shard's. Per-shard HIP-event times of every trace launch and
+    render of the K frames are reported beside it."""
+    devices = plan["devices"]
+    n = len(devices)
+    have = fr.device_count()
+    if have < max(devices) + 1:
+        raise SystemExit(f"bench.py --gpus {n}: devices {devices} requested, {have} present "
+                         f"(FR_BENCH_DEVICES=0,0,... rehearses an {n}-shard run on one device)")
+    rehearsal = len(set(devices)) < n
+
+    rendered = [False]
+
+    def sync_all():
+        if rendered[0]:
+            mc.sync()
+        if torch.cuda.is_available():
+            for d in sorted(set(devices)):
+                torch.cuda.synchronize(d)
+
+    scene = fr.Scene.from_file(fr.scene_path(SCENE), WIDTH, HEIGHT)
+    cam = scene.camera
+    kinds = scene_kinds(fr, scene)
+    mc = fr.MultiContext(devices)
+    params = fr.make_params(WIDTH, HEIGHT, SPP, DEPTH, SEED, scene_jit=not a.no_scene_jit)
+    ctxs = [mc.context(i) for i in range(n)]
+    tp = time.perf_counter()
+    jits = [c.prepare(scene, cam, fr.make_params(WIDTH, HEIGHT, SPP, DEPTH, SEED, shard_index=i, shard_count=n,
+                                                 scene_jit=not a.no_scene_jit)) for i, c in enumerate(ctxs)]
+    prepare_ms = (time.perf_counter() - tp) * 1e3
+    for _ in range(a.warmup):
+        mc.render(scene, cam, params)
+        rendered[0] = True
+        if a.sync_each:
+            mc.sync()
+    if a.warmup:
+        sync_all()
+    for c in ctxs:
+        c.trace_log(True)
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        mc.render(scene, cam, params)
+        rendered[0] = True
+        if a.sync_each:
+            mc.sync()
+    sync_all()  # every shard's last gather has landed
+    elapsed = time.perf_counter() - t0
+    total = mc.sync()
+    shards = []
+    for i, c in enumerate(ctxs):
+        st = c.sync()
+        launches_ms = c.trace_log_read()
+        frames_ms = c.trace_log_read(frames=True)
+        c.trace_log(False)
+        shards.append({"shard": i, "device": devices[i], "samples": st["samples"], "segments": st["segments"],
+                       "hits": st["hits"], "scatters": st["scatters"], "trace_launches": st["trace_launches"],
+                       "occupancy": st["occupancy"],
+                       "trace_ms_per_launch": round(sum(launches_ms) / max(1, len(launches_ms)), 4),
+                       "trace_ms_min_max": [round(min(launches_ms), 4), round(max(launches_ms), 4)]
+                       if launches_ms else None,
+                       "frame_span_ms": round(sum(frames_ms) / max(1, len(frames_ms)), 4),
+                       "launches_logged": len(launches_ms)})
+    mean, _ = mc.frame()
+    value = total["samples"] * a.steps / elapsed / 1e6
+    slow = max(shards, key=lambda s: s["trace_ms_per_launch"] * s["trace_launches"])
+    launches = max(1, slow["trace_launches"])
+    # a shard's consecutive traces may overlap (frame pipeline): cap at the step time
+    launch_ms = min(slow["trace_ms_per_launch"], elapsed / max(1, a.steps) * 1e3)
+    pixels = len(shard_rows(HEIGHT, slow["shard"], n)) * WIDTH
+    roof, hbm = rooflines({k: slow[k] for k in ("segments", "hits", "scatters", "samples")}, kinds, pixels,
+                          len(scene), launches, launch_ms)
+    roof["shard"] = slow["shard"]
+    out = base_line(a, n, value, elapsed, f"row-strips x{n}, one process, fr_mctx over devices {devices}")
+    out.update({
+        "launch": "one process (fr_mctx), no launcher" + (" — REHEARSAL: devices repeat, timing is not an "
+                                                           "N-GPU measurement" if rehearsal else ""),
+        "rehearsal": rehearsal,
+        "step": "one frame: every shard's render + D2H gather of its f32 means and u8 image into one page-locked "
+                "host frame",
+        "host_sync": "each step" if a.sync_each else "after the K steps (frames streamed back to back)",
+        "segments_per_sample": round(total["segments"] / max(1, total["samples"]), 4),
+        "scatters_per_sample": round(total["scatters"] / max(1, total["samples"]), 4),
+        "trace_kernel_ms_per_launch_max_shard": slow["trace_ms_per_launch"],
+        "trace_kernel_ms_per_launch_min_shard": min(s["trace_ms_per_launch"] for s in shards),
+        "shards": shards,
+        "timing_source": "wall clock over the K frames (all devices synchronised on both sides); per-shard HIP "
+                         "events around every trace launch and render (fr_ctx_trace_log)",
+        "scene_kernel": {"specialised": all(j["used"] for j in jits),
+                         "hiprtc_compiled": sum(1 for j in jits if j["compiled"]),
+                         "get_ms": [round(j["ms"], 1) for j in jits], "prepare_ms": round(prepare_ms, 1)},
+        "roofline": roof,
+        "hbm_roofline": hbm,
+        "frame_sha256_16": frame_hash(mean),
+    })
+    mc.close()
+    return out
+
+
+def run_rank(a, plan, torch, fr):
+    """N = 1, or one rank of a torch.distributed.run launch (one process per GPU)."""
+    rank, world, local = plan["rank"], plan["world"], plan["devices"][0]
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    barrier = Barrier(world)
+    scene = fr.Scene.from_file(fr.scene_path(SCENE), WIDTH, HEIGHT)
+    cam = scene.camera
+    n_prims = len(scene)
+    kinds = scene_kinds(fr, scene)
     params = fr.make_params(WIDTH, HEIGHT, SPP, DEPTH, SEED, shard_index=rank, shard_count=world,
                             scene_jit=not a.no_scene_jit)
     ctx = fr.RenderContext(local)
@@ -484,43 +655,23 @@ def main():
     trace_ms = launch_ms * launches                            # trace_kernel launches of one frame
     kernel_ms_max = barrier.max(kernel_ms)
     total_segs = barrier.sum(counts["segments"] * n)
-
-    # rooflines of the dominant kernel (trace_kernel), per launch on this rank
     pixels = len(shard_rows(HEIGHT, rank, world)) * WIDTH
-    c = flop_constants()
-    flops_launch = algorithmic_flops(c, counts, kinds, pixels) / launches
-    tflops = flops_launch / (launch_ms * 1e-3) / 1e12
-    bytes_launch = algorithmic_bytes(pixels, n_prims) / launches
-    gbs = bytes_launch / (launch_ms * 1e-3) / 1e9
 
     checksum = None
-    if a.verify:
+    if a.verify or world == 1:
         frame_img = gather_frame(frame.mean, rank, world, HEIGHT)
         if rank == 0:
-            import hashlib
-            checksum = hashlib.sha256(frame_img.tobytes()).hexdigest()[:16]
+            checksum = frame_hash(frame_img)
     if rank != 0:
-        return
+        return None
     pmc = pmc_in_run(scene_jit=jit["used"]) if (world == 1 and not a.no_pmc) else {}
     issue = valu_issue(pmc)
     traffic = hbm_traffic(pmc)
     value = total_samples / elapsed / 1e6
-    out = {
-        "metric": "Msamples/sec (pixels×spp) at 1920×1080, 256 spp, 8 bounces; 1/2/4/8 GPU",
-        "value": round(value, 3),
-        "unit": "Msamples/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "reference scene file scenes/scene_08.json (bundled), fixed RNG seed 0x5EED",
-        "config": {"workload": f"{SCENE} {WIDTH}x{HEIGHT} {SPP}spp {DEPTH} bounces (BASELINE config 3)",
-                   "scene": SCENE, "width": WIDTH, "height": HEIGHT, "spp": SPP, "max_depth": DEPTH, "seed": SEED,
-                   "parallelism": f"row-strips x{world}"},
+    roof, hbm = rooflines(counts, kinds, pixels, n_prims, launches, launch_ms, traffic, issue)
+    out = base_line(a, world, value, elapsed, f"row-strips x{world}")
+    out.update({
+        "launch": "single process" if world == 1 else f"torch.distributed.run, {world} ranks (one process per GPU)",
         "step": "render of the rank's strips + D2H gather of its f32 means and u8 image into pinned host memory",
         "host_sync": "each step" if a.sync_each else "after the K steps (frames streamed back to back)",
         # a frame's span, its trace's start to its sum's end: frames overlap under the frame
@@ -541,17 +692,9 @@ def main():
                          "get_ms": round(jit["ms"], 1), "prepare_ms": round(prepare_ms, 1),
                          "what": "trace_kernel compiled for this scene's records (FR_FLAG_SCENE_JIT, jit.cpp), "
                                  "before the warm-up; same image bits as the compiled-in kernel"},
-        "roofline": {"bound": "valu", "achieved": round(tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(tflops / FP32_PEAK_TFLOPS, 5), "traffic": round(traffic) if traffic else None,
-                     "peak_no_fma": NO_FMA_PEAK_TOPS, "frac_no_fma": round(tflops / NO_FMA_PEAK_TOPS, 5),
-                     "peak_no_fma_rule": "1024 SIMDs x 32 lanes/clk x 2.4 GHz (no contraction: 1 op per lane-slot)",
-                     "kernel": "trace_kernel", "flops_per_launch": round(flops_launch),
-                     "flop_model": "fo-rma_amd/csrc/flops.h x exact counters", "valu_issue": issue},
-        "hbm_roofline": {"bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gbs / HBM_PEAK_GBS, 8), "bytes_per_launch": round(bytes_launch),
-                         "traffic": round(traffic) if traffic else None,
-                         "measured_gbs": round(traffic / (launch_ms * 1e-3) / 1e9, 2) if traffic else None},
-    }
+        "roofline": roof,
+        "hbm_roofline": hbm,
+    })
     if pmc:
         out["pmc"] = pmc
     if checksum:
@@ -563,9 +706,39 @@ def main():
             out["cpu_baseline"]["c1"] = config_c1(ctx)
         except Exception as e:  # reported in the line; the headline above stands on its own
             out["cpu_baseline"]["c1"] = {"error": f"{type(e).__name__}: {e}"}
-    print(json.dumps(out), flush=True)
     frame.close()
     ctx.close()
+    return out
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    # 20 frames (0.35 s of GPU time at N = 1): the frame pipeline's steady state, in which a
+    # frame's sum runs beside the next frame's trace (DESIGN.md §4.5b); the first and last
+    # frames' sums are inside the timed region too
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--verify", action="store_true", help="stitch the frame on rank 0 and report a checksum")
+    ap.add_argument("--sync-each", action="store_true", help="wait for each frame's stats before the next")
+    ap.add_argument("--no-scene-jit", action="store_true",
+                    help="run the compiled-in trace kernel instead of the scene-specialised one (same image)")
+    return ap.parse_args(argv)
+
+
+def main():
+    a = parse_args()
+    plan = launch_plan(a.gpus)
+    import torch
+
+    import forma_rt as fr  # after torch, so one HIP runtime serves both
+
+    out = run_mctx(a, plan, torch, fr) if plan["mode"] == "mctx" else run_rank(a, plan, torch, fr)
+    if out is not None:
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

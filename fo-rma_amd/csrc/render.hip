@@ -674,6 +674,9 @@ static std::string jit_defines() {
 #ifdef FR_NO_UNROLL_NIB
   d += "#define FR_NO_UNROLL_NIB\n";
 #endif
+#ifdef FR_PROF
+  d += "#define FR_PROF\n";  // section clocks go to the launch's counters, not device globals
+#endif
   return d;
 }
 
@@ -1096,7 +1099,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   {
     const char* je = getenv("FR_SCENE_JIT");
     const bool want = je && *je ? strcmp(je, "0") != 0 : (p->flags & FR_FLAG_SCENE_JIT) != 0;
-#if defined(FR_DIAG) || defined(FR_PROF)
+#if defined(FR_DIAG)
     const bool build_ok = false;  // diagnostics builds keep their device globals in this library
 #else
     const bool build_ok = true;

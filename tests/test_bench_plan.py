@@ -1,0 +1,57 @@
+"""bench.py's launch logic on CPU (no device): how `--gpus N` maps onto processes and
+devices (bench.launch_plan), and the argument parser the driver's command lines use."""
+import pytest
+
+import bench
+
+
+def test_single_gpu_default():
+    p = bench.launch_plan(1, {})
+    assert p == {"mode": "single", "rank": 0, "world": 1, "devices": [0]}
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_plain_command_drives_all_devices_in_one_process(n):
+    p = bench.launch_plan(n, {})
+    assert p["mode"] == "mctx" and p["world"] == 1 and p["devices"] == list(range(n))
+
+
+@pytest.mark.parametrize("spec,n,devs", [("0,0", 2, [0, 0]), ("0,0,0,0,0,0,0,0", 8, [0] * 8), ("3", 1, [3]),
+                                         (" 1, 0 ", 2, [1, 0])])
+def test_rehearsal_devices(spec, n, devs):
+    p = bench.launch_plan(n, {"FR_BENCH_DEVICES": spec})
+    assert p["devices"] == devs
+    assert p["mode"] == ("mctx" if n > 1 else "single")
+
+
+@pytest.mark.parametrize("spec,n", [("0,0,0", 2), ("0", 2), ("-1,0", 2)])
+def test_rehearsal_device_list_must_match(spec, n):
+    with pytest.raises(SystemExit):
+        bench.launch_plan(n, {"FR_BENCH_DEVICES": spec})
+
+
+def test_torchrun_ranks():
+    env = {"RANK": "3", "WORLD_SIZE": "4", "LOCAL_RANK": "3"}
+    assert bench.launch_plan(4, env) == {"mode": "ranks", "rank": 3, "world": 4, "devices": [3]}
+    # every rank on one device (rehearsal under the launcher)
+    assert bench.launch_plan(4, dict(env, FR_BENCH_DEVICE="0"))["devices"] == [0]
+    with pytest.raises(SystemExit):
+        bench.launch_plan(8, env)  # --gpus disagrees with the launcher
+
+
+def test_bad_gpu_count():
+    with pytest.raises(SystemExit):
+        bench.launch_plan(0, {})
+
+
+def test_parse_args_driver_command_line():
+    a = bench.parse_args(["--gpus", "8", "--steps", "5", "--warmup", "1"])
+    assert (a.gpus, a.steps, a.warmup, a.no_scene_jit) == (8, 5, 1, False)
+    a = bench.parse_args([])
+    assert (a.gpus, a.steps, a.warmup) == (1, 20, 2)
+
+
+def test_frame_hash_is_the_rehearsal_checksum():
+    import numpy as np
+    m = np.zeros((4, 5, 3), np.float32)
+    assert bench.frame_hash(m) == bench.frame_hash(m.copy()) and len(bench.frame_hash(m)) == 16
