@@ -9,9 +9,17 @@
 // per segment. The tests, their order and their arithmetic are the list loop's, so the
 // image is the same bits (tests/test_gpu_parity.py::test_scene_jit_*). DESIGN.md §4.11.
 //
-// Modules are cached per process (device, key) and code objects on disk
-// (FR_JIT_CACHE, default $XDG_CACHE_HOME/forma_rt or ~/.cache/forma_rt; "0" disables),
-// keyed by a hash of the embedded sources, defines, kernel name, records and target.
+// Where the code comes from (one code object per key, shared by every device of an arch):
+//   1. this process's code cache (built or read earlier; a module per device on top);
+//   2. the disk cache (FR_JIT_CACHE, default $XDG_CACHE_HOME/forma_rt or ~/.cache/forma_rt;
+//      "0" disables), keyed by a hash of the embedded sources, the hiprtc options, the
+//      hiprtc and HIP runtime versions, the defines, the kernel name, the records and the
+//      target. A file that fails to load is deleted and compiled again once;
+//   3. hiprtc: on the caller's thread when it waits (fr_ctx_prepare, FR_FLAG_SCENE_JIT_WAIT),
+//      else on one background worker thread while renders run the compiled-in kernel.
+// Bounds: at most kMaxModules loaded modules (least recently used unloaded first, after its
+// device drains), kMaxCode code objects in memory and kMaxDiskFiles files on disk.
+#include <dirent.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 #include <stdio.h>
@@ -20,10 +28,15 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "internal.h"
@@ -33,13 +46,19 @@
 namespace fr {
 namespace {
 
-struct Module {
-  hipModule_t mod = nullptr;
-  hipFunction_t fn = nullptr;
-};
+constexpr size_t kMaxModules = 64;    // loaded (device, key) modules per process
+constexpr size_t kMaxCode = 128;      // code objects held in memory per process
+constexpr size_t kMaxDiskFiles = 256; // .hsaco files kept in the disk cache
 
-std::mutex g_mu;
-std::map<std::string, Module> g_modules;  // (device, key) -> loaded module
+// the Makefile's device numerics flags: part of the parity contract, and of
+// the cache key
+const char* const kOpts[] = {"-O3",
+                             "-std=c++17",
+                             "-ffp-contract=off",
+                             "-fno-fast-math",
+                             "-fhip-fp32-correctly-rounded-divide-sqrt",
+                             "-fno-gpu-flush-denormals-to-zero",
+                             "-fno-slp-vectorize"};
 
 uint64_t fnv1a(const void* p, size_t n, uint64_t h) {
   const unsigned char* b = static_cast<const unsigned char*>(p);
@@ -57,6 +76,37 @@ std::string hex_key(const std::string& text) {
   char buf[40];
   snprintf(buf, sizeof buf, "%016llx%016llx", static_cast<unsigned long long>(a), static_cast<unsigned long long>(b));
   return buf;
+}
+
+// FR_JIT_OPTS: extra compiler options, space-separated (A/B experiments only)
+std::vector<std::string> extra_opts() {
+  std::vector<std::string> extra;
+  if (const char* e = getenv("FR_JIT_OPTS")) {
+    std::string cur;
+    for (const char* c = e;; ++c) {
+      if (*c == ' ' || *c == '\0') {
+        if (!cur.empty()) extra.push_back(cur);
+        cur.clear();
+        if (!*c) break;
+      } else {
+        cur += *c;
+      }
+    }
+  }
+  return extra;
+}
+
+// What else decides the code object besides the sources and the records: the option list,
+// the compiler (hiprtc) and runtime versions
+std::string toolchain_tag() {
+  std::string t = "opts:";
+  for (const char* o : kOpts) t += std::string(o) + " ";
+  for (const std::string& o : extra_opts()) t += o + " ";
+  int maj = 0, min = 0, rt = 0;
+  if (hiprtcVersion(&maj, &min) == HIPRTC_SUCCESS) t += "\nhiprtc:" + std::to_string(maj) + "." + std::to_string(min);
+  if (hipRuntimeGetVersion(&rt) == hipSuccess) t += "\nhip:" + std::to_string(rt);
+  t += "\nhip_build:" + std::to_string(HIP_VERSION);
+  return t;
 }
 
 std::string cache_dir() {
@@ -91,13 +141,39 @@ bool read_file(const std::string& path, std::vector<char>& out) {
   return ok;
 }
 
-void write_file_atomic(const std::string& path, const std::vector<char>& data) {
+// The file appears under `path` only when every byte reached the disk: a failed write,
+// flush or close (a full disk) leaves no truncated code object behind.
+bool write_file_atomic(const std::string& path, const std::vector<char>& data) {
   const std::string tmp = path + ".tmp." + std::to_string(getpid());
   FILE* f = fopen(tmp.c_str(), "wb");
-  if (!f) return;  // an unwritable cache only costs the next process a compile
-  const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
-  fclose(f);
-  if (!ok || rename(tmp.c_str(), path.c_str()) != 0) unlink(tmp.c_str());
+  if (!f) return false;  // an unwritable cache only costs the next process a compile
+  bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
+  ok = fflush(f) == 0 && ok;
+  ok = fsync(fileno(f)) == 0 && ok;
+  ok = fclose(f) == 0 && ok;
+  if (!ok || rename(tmp.c_str(), path.c_str()) != 0) {
+    unlink(tmp.c_str());
+    return false;
+  }
+  return true;
+}
+
+// Keep at most kMaxDiskFiles code objects in the cache directory: the oldest go first.
+void prune_disk(const std::string& dir) {
+  DIR* d = opendir(dir.c_str());
+  if (!d) return;
+  std::vector<std::pair<time_t, std::string>> files;
+  while (const dirent* e = readdir(d)) {
+    const std::string name = e->d_name;
+    if (name.size() < 7 || name.compare(name.size() - 6, 6, ".hsaco") != 0) continue;
+    struct stat s;
+    const std::string p = dir + "/" + name;
+    if (stat(p.c_str(), &s) == 0) files.emplace_back(s.st_mtime, p);
+  }
+  closedir(d);
+  if (files.size() <= kMaxDiskFiles) return;
+  std::sort(files.begin(), files.end());
+  for (size_t i = 0; i + kMaxDiskFiles < files.size(); ++i) unlink(files[i].second.c_str());
 }
 
 // hiprtc: the embedded trace_kernel.h with the prelude's defines and records
@@ -108,32 +184,14 @@ int compile(const std::string& arch, const std::string& prelude, const char* nam
   if (hiprtcCreateProgram(&prog, src.c_str(), "fr_scene_kernel.hip", jit_src::kCount, jit_src::kBodies,
                           jit_src::kNames) != HIPRTC_SUCCESS)
     return set_error(FR_EHIP, "hiprtcCreateProgram failed");
-  hiprtcAddNameExpression(prog, name_expr);
-  // the Makefile's device numerics flags: part of the parity contract
-  const std::string arch_opt = "--offload-arch=" + arch;
-  const char* opts[] = {arch_opt.c_str(),
-                        "-O3",
-                        "-std=c++17",
-                        "-ffp-contract=off",
-                        "-fno-fast-math",
-                        "-fhip-fp32-correctly-rounded-divide-sqrt",
-                        "-fno-gpu-flush-denormals-to-zero",
-                        "-fno-slp-vectorize"};
-  std::vector<const char*> all(opts, opts + sizeof(opts) / sizeof(opts[0]));
-  // FR_JIT_OPTS: extra compiler options, space-separated (A/B experiments only)
-  std::vector<std::string> extra;
-  if (const char* e = getenv("FR_JIT_OPTS")) {
-    std::string cur;
-    for (const char* c = e;; ++c) {
-      if (*c == ' ' || *c == '\0') {
-        if (!cur.empty()) extra.push_back(cur);
-        cur.clear();
-        if (!*c) break;
-      } else {
-        cur += *c;
-      }
-    }
+  if (hiprtcAddNameExpression(prog, name_expr) != HIPRTC_SUCCESS) {
+    hiprtcDestroyProgram(&prog);
+    return set_error(FR_EHIP, "hiprtcAddNameExpression(%s) failed", name_expr);
   }
+  const std::string arch_opt = "--offload-arch=" + arch;
+  std::vector<const char*> all{arch_opt.c_str()};
+  for (const char* o : kOpts) all.push_back(o);
+  const std::vector<std::string> extra = extra_opts();
   for (const std::string& x : extra) all.push_back(x.c_str());
   const hiprtcResult r = hiprtcCompileProgram(prog, static_cast<int>(all.size()), all.data());
   if (r != HIPRTC_SUCCESS) {
@@ -152,7 +210,7 @@ int compile(const std::string& arch, const std::string& prelude, const char* nam
   size_t n = 0;
   hiprtcGetCodeSize(prog, &n);
   code.resize(n);
-  hiprtcGetCode(prog, code.data());
+  if (n) hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
   // FR_JIT_DUMP=path keeps the code object (llvm-objdump / resource inspection)
   if (const char* dump = getenv("FR_JIT_DUMP"); dump && *dump && n) write_file_atomic(dump, code);
@@ -173,6 +231,18 @@ std::string mangled(const int* targs, const bool* is_bool, int n) {
   return m + "EEvNS_5KArgsE";
 }
 
+// A fresh compile whose kernel name is the one the loader looks up (checked before the code
+// object is cached anywhere).
+int compile_checked(const std::string& arch, const std::string& prelude, const std::string& name_expr,
+                    const std::string& mname, std::vector<char>& code) {
+  std::string lowered;
+  const int rc = compile(arch, prelude, name_expr.c_str(), code, &lowered);
+  if (rc) return rc;
+  if (lowered != mname)
+    return set_error(FR_EHIP, "scene kernel name %s, expected %s", lowered.c_str(), mname.c_str());
+  return FR_OK;
+}
+
 // the host build's tuning/contract macros, then the scene's records
 std::string make_prelude(const JitSpec& spec) {
   std::string prelude = spec.defines;
@@ -189,25 +259,114 @@ std::string make_prelude(const JitSpec& spec) {
   return prelude + "\n";
 }
 
-}  // namespace
+struct CodeEntry {
+  enum State { kCompiling, kReady, kFailed } state = kCompiling;
+  std::shared_ptr<const std::vector<char>> code;
+  std::string error;
+  bool from_disk = false;
+  uint64_t used = 0;
+};
 
-int jit_compile_probe(const char* arch, const JitSpec& spec, size_t* code_bytes, double* ms) {
-  const auto t0 = std::chrono::steady_clock::now();
-  std::vector<char> code;
-  std::string lowered;
-  const int rc = compile(arch, make_prelude(spec), spec.name_expr, code, &lowered);
-  if (rc) return rc;
-  const std::string mname = mangled(spec.targs, spec.targ_bool, spec.n_targs);
-  if (lowered != mname)
-    return set_error(FR_EHIP, "scene kernel name %s, expected %s", lowered.c_str(), mname.c_str());
-  if (code_bytes) *code_bytes = code.size();
-  if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  return FR_OK;
+struct Module {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  int device = 0;
+  uint64_t used = 0;
+};
+
+struct Job {  // a background compile: everything copied, nothing borrowed from the caller
+  std::string key, arch, prelude, name_expr, mname, path;
+};
+
+// Process-wide state. The background worker is joined when the library is unloaded (process
+// exit): a compile still running then finishes first, so hiprtc never runs while its library
+// is being torn down. Queued compiles that have not started are dropped.
+class Registry {
+ public:
+  std::mutex mu;
+  std::condition_variable cv;                 // an entry left kCompiling, or a job arrived
+  std::map<std::string, CodeEntry> code;      // key -> code object
+  std::map<std::string, Module> modules;      // "device:key" -> loaded module
+  std::deque<Job> jobs;
+  int compiling = 0;                          // entries in kCompiling
+  uint64_t tick = 0;
+  bool stop = false;
+  std::thread worker;
+
+  ~Registry() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    if (worker.joinable()) worker.join();
+    // modules are left to the runtime's own teardown: at exit it may already be gone
+  }
+
+  void finish(const std::string& key, int rc, std::vector<char>&& bytes, const std::string& err, bool from_disk) {
+    auto it = code.find(key);
+    if (it == code.end()) return;
+    if (it->second.state == CodeEntry::kCompiling) --compiling;
+    if (rc == FR_OK) {
+      it->second.state = CodeEntry::kReady;
+      it->second.code = std::make_shared<const std::vector<char>>(std::move(bytes));
+      it->second.from_disk = from_disk;
+    } else {
+      it->second.state = CodeEntry::kFailed;
+      it->second.error = err;
+    }
+    it->second.used = ++tick;
+    trim_code();
+    cv.notify_all();
+  }
+
+  void trim_code() {  // drop the least recently used ready code objects beyond kMaxCode
+    while (code.size() > kMaxCode) {
+      auto victim = code.end();
+      for (auto it = code.begin(); it != code.end(); ++it)
+        if (it->second.state != CodeEntry::kCompiling && (victim == code.end() || it->second.used < victim->second.used))
+          victim = it;
+      if (victim == code.end()) return;
+      code.erase(victim);
+    }
+  }
+
+  void run_worker() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || !jobs.empty(); });
+      if (stop) {
+        for (const Job& j : jobs) finish(j.key, FR_EHIP, {}, "abandoned at exit", false);
+        jobs.clear();
+        return;
+      }
+      Job j = std::move(jobs.front());
+      jobs.pop_front();
+      lk.unlock();
+      std::vector<char> bytes;
+      const int rc = compile_checked(j.arch, j.prelude, j.name_expr, j.mname, bytes);
+      const std::string err = rc ? fr_last_error() : "";
+      if (rc == FR_OK && !j.path.empty() && write_file_atomic(j.path, bytes)) prune_disk(j.path.substr(0, j.path.rfind('/')));
+      lk.lock();
+      finish(j.key, rc, std::move(bytes), err, false);
+    }
+  }
+
+  void enqueue(Job&& j) {  // caller holds mu
+    jobs.push_back(std::move(j));
+    if (!worker.joinable()) worker = std::thread([this] { run_worker(); });
+    cv.notify_all();
+  }
+};
+
+Registry& reg() {
+  static Registry r;
+  return r;
 }
 
 // The device's target name (gcnArchName), queried once per device: every render of a
 // scene-specialised frame looks its kernel up, and the property query is not free.
-static std::string device_arch(int device) {
+std::string device_arch(int device) {
   static std::mutex mu;
   static std::map<int, std::string> arch;
   std::lock_guard<std::mutex> g(mu);
@@ -218,47 +377,165 @@ static std::string device_arch(int device) {
   return arch[device] = prop.gcnArchName;
 }
 
-int jit_trace_kernel(int device, const JitSpec& spec, hipFunction_t* out, JitStats* stats) {
+const std::string& toolchain() {
+  static const std::string t = toolchain_tag();
+  return t;
+}
+
+// Unload a module evicted from the table once its device has drained: a launch of it may
+// still be queued on a stream (the evicted module is the least recently resolved one, so
+// no render is between resolving it and launching it).
+void unload_evicted(const Module& m) {
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(m.device);
+  (void)hipDeviceSynchronize();
+  (void)hipModuleUnload(m.mod);
+  if (cur >= 0) (void)hipSetDevice(cur);
+}
+
+}  // namespace
+
+int jit_compile_probe(const char* arch, const JitSpec& spec, size_t* code_bytes, double* ms) {
   const auto t0 = std::chrono::steady_clock::now();
+  std::vector<char> code;
+  const int rc = compile_checked(arch, make_prelude(spec), spec.name_expr, mangled(spec.targs, spec.targ_bool, spec.n_targs),
+                                 code);
+  if (rc) return rc;
+  if (code_bytes) *code_bytes = code.size();
+  if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return FR_OK;
+}
+
+int jit_wait_all() {
+  Registry& R = reg();
+  std::unique_lock<std::mutex> lk(R.mu);
+  R.cv.wait(lk, [&] { return R.compiling == 0; });
+  return FR_OK;
+}
+
+int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* out, JitStats* stats) {
+  const auto t0 = std::chrono::steady_clock::now();
+  JitStats st;
+  auto done = [&](int state) {
+    st.state = state;
+    st.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = st;
+    return FR_OK;
+  };
+  *out = nullptr;
   const std::string arch = device_arch(device);
   if (arch.empty()) return set_error(FR_EHIP, "hipGetDeviceProperties failed");
   const std::string prelude = make_prelude(spec);
-  const char* xo = getenv("FR_JIT_OPTS");
-  const std::string key = hex_key(std::string(jit_src::kHash) + "\n" + arch + "\n" + spec.name_expr + "\n" + prelude +
-                                  (xo ? xo : ""));
+  const std::string key =
+      hex_key(std::string(jit_src::kHash) + "\n" + arch + "\n" + spec.name_expr + "\n" + toolchain() + "\n" + prelude);
   const std::string mkey = std::to_string(device) + ":" + key;
-  std::lock_guard<std::mutex> g(g_mu);
-  auto it = g_modules.find(mkey);
-  if (it != g_modules.end()) {
-    *out = it->second.fn;
-    if (stats) *stats = JitStats{0.0, 0, 1};
-    return FR_OK;
-  }
-  std::vector<char> code;
-  int cached = 0;
+  const std::string mname = mangled(spec.targs, spec.targ_bool, spec.n_targs);
   const std::string dir = cache_dir();
   const std::string path = dir.empty() ? "" : dir + "/" + key + ".hsaco";
-  if (!path.empty() && read_file(path, code)) cached = 1;
-  if (!cached) {
-    const int rc = compile(arch, prelude, spec.name_expr, code);
-    if (rc) return rc;
-    if (!path.empty()) write_file_atomic(path, code);
+  Registry& R = reg();
+  std::unique_lock<std::mutex> lk(R.mu);
+  auto mi = R.modules.find(mkey);
+  if (mi != R.modules.end()) {
+    mi->second.used = ++R.tick;
+    *out = mi->second.fn;
+    st.reused = 1;
+    return done(FR_JIT_USED);
   }
-  Module m;
-  hipError_t e = hipModuleLoadData(&m.mod, code.data());
-  if (e != hipSuccess) return set_error(FR_EHIP, "hipModuleLoadData (scene kernel): %s", hipGetErrorString(e));
-  const std::string mname = mangled(spec.targs, spec.targ_bool, spec.n_targs);
-  e = hipModuleGetFunction(&m.fn, m.mod, mname.c_str());
-  if (e != hipSuccess) {
-    (void)hipModuleUnload(m.mod);
-    return set_error(FR_EHIP, "hipModuleGetFunction(%s): %s", mname.c_str(), hipGetErrorString(e));
+  // attempt 0 may take the disk cache; a disk file that does not load is deleted and the
+  // kernel compiled once more (attempt 1)
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    auto it = R.code.find(key);
+    if (it == R.code.end()) {
+      R.code[key];  // kCompiling: later requests for this key wait (or pend) on it
+      ++R.compiling;
+      lk.unlock();
+      std::vector<char> bytes;
+      if (attempt == 0 && !path.empty() && read_file(path, bytes)) {
+        lk.lock();
+        R.finish(key, FR_OK, std::move(bytes), "", true);
+      } else if (wait) {
+        const int rc = compile_checked(arch, prelude, spec.name_expr, mname, bytes);
+        const std::string err = rc ? fr_last_error() : "";
+        if (rc == FR_OK && !path.empty() && write_file_atomic(path, bytes)) prune_disk(dir);
+        st.compiled = 1;
+        lk.lock();
+        R.finish(key, rc, std::move(bytes), err, false);
+      } else {
+        lk.lock();
+        R.enqueue(Job{key, arch, prelude, spec.name_expr, mname, path});
+        st.compiled = 1;
+        return done(FR_JIT_PENDING);
+      }
+      it = R.code.find(key);
+      if (it == R.code.end()) return set_error(FR_EHIP, "scene kernel code object evicted while loading");
+    }
+    if (it->second.state == CodeEntry::kCompiling) {
+      if (!wait) return done(FR_JIT_PENDING);
+      R.cv.wait(lk, [&] {
+        auto e = R.code.find(key);
+        return e == R.code.end() || e->second.state != CodeEntry::kCompiling;
+      });
+      it = R.code.find(key);
+      if (it == R.code.end()) continue;  // evicted meanwhile: look again
+    }
+    if (it->second.state == CodeEntry::kFailed) {
+      if (!wait) {
+        st.error = it->second.error;
+        return done(FR_JIT_FAILED);
+      }
+      return set_error(FR_EHIP, "%s", it->second.error.c_str());
+    }
+    it->second.used = ++R.tick;
+    const std::shared_ptr<const std::vector<char>> bytes = it->second.code;
+    const bool from_disk = it->second.from_disk;
+    lk.unlock();
+    Module m;
+    m.device = device;
+    hipError_t e = hipModuleLoadData(&m.mod, bytes->data());
+    if (e == hipSuccess) {
+      e = hipModuleGetFunction(&m.fn, m.mod, mname.c_str());
+      if (e != hipSuccess) (void)hipModuleUnload(m.mod);
+    }
+    lk.lock();
+    if (e != hipSuccess) {
+      if (from_disk && attempt == 0) {
+        // a truncated or foreign file in the cache: remove it and build the kernel afresh
+        if (!path.empty()) unlink(path.c_str());
+        R.code.erase(key);
+        continue;
+      }
+      return set_error(FR_EHIP, "loading the scene kernel %s: %s", mname.c_str(), hipGetErrorString(e));
+    }
+    auto prev = R.modules.find(mkey);
+    if (prev != R.modules.end()) {  // another thread loaded it meanwhile: keep the first
+      lk.unlock();
+      (void)hipModuleUnload(m.mod);
+      lk.lock();
+      prev = R.modules.find(mkey);
+      if (prev != R.modules.end()) {
+        prev->second.used = ++R.tick;
+        *out = prev->second.fn;
+        return done(FR_JIT_USED);
+      }
+      continue;
+    }
+    m.used = ++R.tick;
+    R.modules[mkey] = m;
+    *out = m.fn;
+    std::vector<Module> evicted;
+    while (R.modules.size() > kMaxModules) {
+      auto victim = R.modules.begin();
+      for (auto v = R.modules.begin(); v != R.modules.end(); ++v)
+        if (v->second.used < victim->second.used) victim = v;
+      evicted.push_back(victim->second);
+      R.modules.erase(victim);
+    }
+    lk.unlock();
+    for (const Module& v : evicted) unload_evicted(v);
+    return done(FR_JIT_USED);
   }
-  g_modules[mkey] = m;  // kept for the process's lifetime (a few hundred KB per scene)
-  *out = m.fn;
-  if (stats)
-    *stats = JitStats{std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
-                      cached ? 0 : 1, 0};
-  return FR_OK;
+  return set_error(FR_EHIP, "scene kernel: no code object after a recompile");
 }
 
 }  // namespace fr

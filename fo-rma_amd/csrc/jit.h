@@ -23,15 +23,26 @@ struct JitSpec {
 };
 
 struct JitStats {
-  double ms;      // wall time of this call (compile or cache load, module load)
-  int compiled;   // 1: hiprtc ran; 0: code object from the disk cache or module reused
-  int reused;     // 1: the module was already loaded in this process
+  double ms = 0.0;   // wall time of this call (cache or module load, or a compile it ran or waited for)
+  int compiled = 0;  // 1: hiprtc ran for this request (in this call, or started in the background)
+  int reused = 0;    // 1: the module was already loaded in this process
+  int state = 0;     // FR_JIT_* (forma_rt.h): USED, PENDING (no kernel yet) or FAILED
+  std::string error; // FAILED: the compiler's message
 };
 
-// The kernel for spec on device (current device must be `device`). FR_OK, or an FR_E*
-// code with fr_last_error() holding hiprtc's log: the caller fails the render (no
-// silent fallback, so a broken run-time build cannot hide behind the generic kernel).
-int jit_trace_kernel(int device, const JitSpec& spec, hipFunction_t* out, JitStats* stats);
+// The scene kernel for spec on `device` (the current device must be `device`).
+// wait = true: compile on this thread if no code object exists (or wait for the background
+// compile of the same key); FR_OK with *out set, or an FR_E* code with fr_last_error()
+// holding hiprtc's log.
+// wait = false: never compiles on this thread. A code object already built (this process)
+// or cached on disk is loaded and returned; otherwise the compile is queued on the
+// background worker and FR_OK returns with *out = nullptr and stats->state PENDING (or
+// FAILED after a failed compile): the caller runs the compiled-in kernel, whose image is
+// the same bits.
+int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* out, JitStats* stats);
+
+// Block until the background worker has no compile queued or running.
+int jit_wait_all();
 
 // hiprtc only, no device (tests): compiles spec for arch and checks that the kernel's
 // lowered name is the one jit_trace_kernel looks up.

@@ -591,6 +591,7 @@ struct fr_ctx {
   // the last render's trace kernel: scene-specialised (jit.h) or compiled in
   bool jit_used = false;
   JitStats jit_stats{};
+  int jit_state = FR_JIT_OFF;
   bool log_on = false;
   std::vector<hipEvent_t> log_ev[2];  // 2 per entry (start, end); reused across logs
   size_t log_n[2] = {0, 0};           // entries logged
@@ -634,11 +635,14 @@ struct Grid {
 // when the caller asks (FR_FLAG_SCENE_JIT or FR_SCENE_JIT=1) and the scene is small.
 struct JitReq {
   bool on = false;
+  bool wait = false;  // compile on this thread if needed (fr_ctx_prepare, FR_FLAG_SCENE_JIT_WAIT)
   int device = 0;
   const DeviceCopy* dc = nullptr;
   bool dry = false;   // fr_ctx_prepare: get the kernel, launch nothing
+  bool resolved = false;     // the lookup ran (once per render: the dry pre-step)
+  hipFunction_t fn = nullptr;  // its result: the scene kernel, or null (compiled-in kernel)
   bool used = false;  // out: the launch ran the scene-specialised kernel
-  JitStats stats{};   // out: its compile / cache-load time
+  JitStats stats{};   // out: the lookup's time and state
 };
 
 // The host build's tuning and contract macros, so the run-time build of trace_kernel.h
@@ -685,15 +689,19 @@ static int launch_persistent(const Grid& g, size_t lds, hipStream_t st, KArgs a,
   auto kern = trace_kernel<KS, HP, KREJ, MAXD, BV, MT, DEFER, MAT>;
   hipFunction_t jfn = nullptr;
   if (!BV && jr && jr->on) {
-    char name[160];
-    snprintf(name, sizeof name, "fr::trace_kernel<%d, %s, %d, %d, %s, %s, %d, %d>", KS, HP ? "true" : "false", KREJ,
-             MAXD, BV ? "true" : "false", MT ? "true" : "false", DEFER, MAT);
-    const int targs[8] = {KS, HP, KREJ, MAXD, BV, MT, DEFER, MAT};
-    const bool tbool[8] = {false, true, false, false, true, true, false, false};
-    const JitSpec spec{name, targs, tbool, 8, jit_defines(), jr->dc->rec_words.data(), jr->dc->n};
-    const int rc = jit_trace_kernel(jr->device, spec, &jfn, &jr->stats);
-    if (rc) return rc;
-    jr->used = true;
+    if (!jr->resolved) {
+      char name[160];
+      snprintf(name, sizeof name, "fr::trace_kernel<%d, %s, %d, %d, %s, %s, %d, %d>", KS, HP ? "true" : "false", KREJ,
+               MAXD, BV ? "true" : "false", MT ? "true" : "false", DEFER, MAT);
+      const int targs[8] = {KS, HP, KREJ, MAXD, BV, MT, DEFER, MAT};
+      const bool tbool[8] = {false, true, false, false, true, true, false, false};
+      const JitSpec spec{name, targs, tbool, 8, jit_defines(), jr->dc->rec_words.data(), jr->dc->n};
+      const int rc = jit_trace_kernel(jr->device, spec, jr->wait, &jr->fn, &jr->stats);
+      if (rc) return rc;
+      jr->resolved = true;
+    }
+    jfn = jr->fn;  // null while the compile is pending (or failed): the compiled-in kernel runs
+    jr->used = jfn != nullptr;
   }
   if (jr && jr->dry) return FR_OK;
   int per_cu = 0;
@@ -1105,11 +1113,14 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     const bool build_ok = true;
 #endif
     jr.on = want && build_ok && !use_bvh && dc->n >= 1 && dc->n <= kJitMaxPrims;
+    // prepare, FR_FLAG_SCENE_JIT_WAIT and the environment's FR_SCENE_JIT=1 wait for the
+    // compile; plain FR_FLAG_SCENE_JIT renders run the compiled-in kernel until it is done
+    jr.wait = dry || (p->flags & FR_FLAG_SCENE_JIT_WAIT) != 0 || (je && *je && strcmp(je, "0") != 0);
   }
   KWork kw;
   kw.counters = cnt;
-  // the scene-specialised kernel is compiled or loaded here, before anything is enqueued,
-  // so a first frame's events do not span the compile
+  // the scene-specialised kernel is looked up here (loaded, or compiled when waiting),
+  // before anything is enqueued, so a first frame's events do not span the compile
   JitStats jit_got{};
   if (jr.on && kp.P) {
     JitReq pre = jr;
@@ -1121,10 +1132,14 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
                       &pre);
     if (rc) return rc;
     jit_got = pre.stats;
+    jr.resolved = pre.resolved;
+    jr.fn = pre.fn;
   }
+  const int jit_state = jr.on && kp.P ? jit_got.state : FR_JIT_OFF;
   if (dry) {
-    c->jit_used = jr.on && kp.P;
+    c->jit_used = jr.on && kp.P && jr.fn != nullptr;
     c->jit_stats = jit_got;
+    c->jit_state = jit_state;
     return FR_OK;
   }
   c->t0 = std::chrono::steady_clock::now();
@@ -1229,6 +1244,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   c->passes = traced;
   c->jit_used = jr.used;
   c->jit_stats = jit_got;
+  c->jit_state = jit_state;
   HIPCHK(hipEventRecord(c->ev1, end_stream));
   if (c->log_on) HIPCHK(log_end(c, 1, end_stream));
   c->last = *p;
@@ -1457,19 +1473,29 @@ int fr_selftest_jit(const char* arch, const uint32_t* rec, uint32_t n, const int
 int fr_ctx_jit_info(fr_ctx* c, int* used, double* ms, int* compiled) {
   if (!c) return set_error(FR_EARG, "fr_ctx_jit_info: null ctx");
   if (used) *used = c->jit_used ? 1 : 0;
-  if (ms) *ms = c->jit_used ? c->jit_stats.ms : 0.0;
-  if (compiled) *compiled = c->jit_used ? c->jit_stats.compiled : 0;
+  if (ms) *ms = c->jit_state != FR_JIT_OFF ? c->jit_stats.ms : 0.0;
+  if (compiled) *compiled = c->jit_state != FR_JIT_OFF ? c->jit_stats.compiled : 0;
   return FR_OK;
 }
+
+int fr_ctx_jit_state(fr_ctx* c, int* state) {
+  if (!c || !state) return set_error(FR_EARG, "fr_ctx_jit_state: null argument");
+  *state = c->jit_state;
+  if (c->jit_state == FR_JIT_FAILED) set_error(FR_EHIP, "%s", c->jit_stats.error.c_str());
+  return FR_OK;
+}
+
+int fr_jit_wait(void) { return jit_wait_all(); }
 
 int fr_ctx_trace_log(fr_ctx* c, int enable) {
   if (!c) return set_error(FR_EARG, "fr_ctx_trace_log: null ctx");
   if (enable) {
     SET_DEVICE(c->device);
-    // the pairs of an earlier log may still be pending on the streams: drain them before
-    // their events are recorded again
+    // the pairs of an earlier log may still be pending on the streams (a pipelined render
+    // records its end on the sum stream): drain them before their events are recorded again
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->stream2));
+    HIPCHK(hipStreamSynchronize(c->stream_sum));
     c->log_n[0] = c->log_n[1] = 0;
   }
   c->log_on = enable != 0;
@@ -1481,6 +1507,7 @@ int fr_ctx_trace_log_read(fr_ctx* c, int which, double* ms, uint32_t cap, uint32
   SET_DEVICE(c->device);
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->stream2));
+  HIPCHK(hipStreamSynchronize(c->stream_sum));  // a pipelined render's end event is recorded there
   *n = static_cast<uint32_t>(c->log_n[which]);
   for (size_t i = 0; i < c->log_n[which] && i < cap && ms; ++i) {
     float t = 0.0f;

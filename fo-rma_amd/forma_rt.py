@@ -27,13 +27,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FORMA_RT_LIB") or os.path.join(HERE, "libforma_rt.so")
 SCENES_DIR = os.path.join(HERE, "scenes")
 
-FR_ABI_VERSION = 5  # include/forma_rt.h FR_ABI_VERSION
+FR_ABI_VERSION = 6  # include/forma_rt.h FR_ABI_VERSION
 FR_OK, FR_EARG, FR_EPARSE, FR_EHIP, FR_ENODEV, FR_ENOMEM = 0, -1, -2, -3, -4, -5
 FR_SPHERE, FR_PLANE, FR_AABB, FR_OBB, FR_STUB, FR_TRIANGLE = 0, 1, 2, 3, 4, 5
 FR_LAMBERTIAN, FR_METAL, FR_DIELECTRIC, FR_LIGHT = 0, 1, 2, 3
 FR_FLAG_WRITE_U8 = 1
 FR_FLAG_MT_BANDS = 2  # save_image_mt semantics (forma_rt.h)
 FR_FLAG_SCENE_JIT = 4  # scene-specialised trace kernel (hiprtc, cached; same image bits)
+FR_FLAG_SCENE_JIT_WAIT = 8  # ... compiled on the render's thread when missing (else in the background)
+FR_JIT_OFF, FR_JIT_USED, FR_JIT_PENDING, FR_JIT_FAILED = 0, 1, 2, 3  # fr_ctx_jit_state
 MAX_DEPTH = 50  # tracer.rs:10
 DEFAULT_SEED = 0x5EED
 
@@ -88,7 +90,7 @@ EXPORTS = (
     "fr_mctx_sync", "fr_mctx_frame", "fr_mctx_download",
     "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_recip",
     "fr_post_process", "fr_post_process_device", "fr_rgb_to_rgba_device", "fr_ctx_jit_info", "fr_selftest_jit",
-    "fr_ctx_prepare",
+    "fr_ctx_prepare", "fr_ctx_jit_state", "fr_jit_wait",
 )
 
 _lib = None
@@ -175,6 +177,9 @@ def lib():
     if hasattr(L, "fr_ctx_jit_info"):  # absent from A/B builds of older sources
         L.fr_ctx_jit_info.argtypes = [vp, P(C.c_int), P(C.c_double), P(C.c_int)]
         L.fr_ctx_prepare.argtypes = [vp, vp, P(FrCamera), P(FrParams)]
+    if hasattr(L, "fr_ctx_jit_state"):  # absent from A/B builds of older sources
+        L.fr_ctx_jit_state.argtypes = [vp, P(C.c_int)]
+        L.fr_jit_wait.argtypes = []
         L.fr_selftest_jit.argtypes = [C.c_char_p, P(C.c_uint32), C.c_uint32, P(C.c_int), P(C.c_size_t), P(C.c_double)]
     _lib = L
     return L
@@ -398,12 +403,19 @@ def scene_path(name):
 
 def make_params(width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, shard_index=0, shard_count=1,
                 write_u8=True, mt_bands=False, scene_jit=False):
+    """scene_jit: False, True (the scene kernel once it is compiled; until then renders run
+    the compiled-in kernel, same bits) or "wait" (compile on the render's thread if needed)."""
     p = FrParams()
     p.width, p.height, p.spp, p.max_depth, p.seed = width, height, spp, max_depth, seed
     p.strip_rows, p.shard_index, p.shard_count = 8, shard_index, shard_count
     p.flags = ((FR_FLAG_WRITE_U8 if write_u8 else 0) | (FR_FLAG_MT_BANDS if mt_bands else 0) |
-               (FR_FLAG_SCENE_JIT if scene_jit else 0))
+               (FR_FLAG_SCENE_JIT if scene_jit else 0) | (FR_FLAG_SCENE_JIT_WAIT if scene_jit == "wait" else 0))
     return p
+
+
+def jit_wait():
+    """Block until no scene-kernel compile is queued or running in this process."""
+    check(lib().fr_jit_wait())
 
 
 class _PinnedBlock:
@@ -507,7 +519,13 @@ class RenderContext:
         that render spent getting it (compile or cache load), "compiled": hiprtc ran}."""
         used, ms, comp = C.c_int(0), C.c_double(0.0), C.c_int(0)
         check(lib().fr_ctx_jit_info(self._h, C.byref(used), C.byref(ms), C.byref(comp)))
-        return {"used": bool(used.value), "ms": ms.value, "compiled": bool(comp.value)}
+        return {"used": bool(used.value), "ms": ms.value, "compiled": bool(comp.value), "state": self.jit_state()}
+
+    def jit_state(self):
+        """FR_JIT_OFF / USED / PENDING / FAILED for the last render (fr_ctx_jit_state)."""
+        s = C.c_int(0)
+        check(lib().fr_ctx_jit_state(self._h, C.byref(s)))
+        return s.value
 
     def trace_log(self, enable=True):
         """Start (or stop) logging every trace-kernel launch's HIP-event duration."""
@@ -665,7 +683,8 @@ class TraceModel:
 
     def render(self, scene, spp, max_depth, seed, mt_bands=False, scene_jit=False):
         """One frame on the model's context: (mean[H,W,3], u8[H,W,3], stats). scene_jit: the
-        trace kernel compiled for the scene (same bits; worth it for many-sample renders)."""
+        trace kernel compiled for the scene once ready (same bits; compiled in the background,
+        so a render never waits for it)."""
         ctx = self.context()
         ctx.render(scene, self.scene.camera, make_params(self.width, self.height, spp, max_depth, seed,
                                                          mt_bands=mt_bands, scene_jit=scene_jit))

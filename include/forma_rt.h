@@ -49,12 +49,14 @@
 extern "C" {
 #endif
 
-#define FR_ABI_VERSION 5 /* 2: fr_stats.trace_launches; FR_TRIANGLE; post effects; FR_FLAG_MT_BANDS
+#define FR_ABI_VERSION 6 /* 2: fr_stats.trace_launches; FR_TRIANGLE; post effects; FR_FLAG_MT_BANDS
                             3: fr_stats.scatters/.occupancy; fr_ctx_download_async, fr_ctx_wait,
                                fr_host_alloc/free; item-major sample buffer
                             4: fr_mctx_* (persistent multi-device context); fr_ctx_trace_log(_read);
                                entry points restore the caller's current HIP device
-                            5: FR_FLAG_SCENE_JIT, fr_ctx_prepare, fr_ctx_jit_info */
+                            5: FR_FLAG_SCENE_JIT, fr_ctx_prepare, fr_ctx_jit_info
+                            6: FR_FLAG_SCENE_JIT compiles in the background (renders never wait),
+                               FR_FLAG_SCENE_JIT_WAIT, fr_ctx_jit_state, fr_jit_wait */
 
 /* error codes */
 #define FR_OK 0
@@ -87,12 +89,21 @@ extern "C" {
    max_depth 50 to match the reference call. */
 #define FR_FLAG_MT_BANDS 2u
 /* Scene-specialised trace kernel (render.hip / jit.cpp): for list-loop scenes of at most 64
-   primitives, compile the kernel once per scene with the primitive records as constants
-   (hiprtc; cached per process and on disk, FR_JIT_CACHE). Same image bits as without the
-   flag; shared slab planes are computed once per segment. The first render of a scene
-   pays the compile (seconds; fr_ctx_jit_info reports it). FR_SCENE_JIT=1 / 0 in the
-   environment forces it on / off for every render. */
+   primitives, the kernel compiled once per scene with the primitive records as constants
+   (hiprtc; one code object per GPU architecture, cached per process and on disk,
+   FR_JIT_CACHE). Same image bits as without the flag; shared slab planes are computed once
+   per segment. A render never waits for the compile: when no code object exists yet it is
+   queued on a background host thread and the render runs the compiled-in kernel
+   (fr_ctx_jit_state says FR_JIT_PENDING); a later render picks the scene kernel up.
+   fr_ctx_prepare, FR_FLAG_SCENE_JIT_WAIT, and FR_SCENE_JIT=1 in the environment wait for it
+   instead (FR_SCENE_JIT=0 turns it off for every render). */
 #define FR_FLAG_SCENE_JIT 4u
+#define FR_FLAG_SCENE_JIT_WAIT 8u /* with FR_FLAG_SCENE_JIT: compile on the render's thread if needed */
+/* fr_ctx_jit_state: which trace kernel the last render (or fr_ctx_prepare) ran */
+#define FR_JIT_OFF 0     /* compiled-in kernel: not asked for, a BVH scene, or > 64 primitives */
+#define FR_JIT_USED 1    /* the scene-specialised kernel */
+#define FR_JIT_PENDING 2 /* asked for, compile still running: the compiled-in kernel ran */
+#define FR_JIT_FAILED 3  /* asked for, compile failed: the compiled-in kernel ran */
 
 /*
  * One primitive, in the order it is tested (list order decides ties, tracer.rs:195-200).
@@ -227,6 +238,11 @@ int fr_ctx_prepare(fr_ctx* ctx, fr_scene* scene, const fr_camera* cam, const fr_
    (FR_FLAG_SCENE_JIT), *ms = the time that render spent getting it (hiprtc compile, disk
    cache load or 0 when already loaded), *compiled = 1 when hiprtc ran. Any may be NULL. */
 int fr_ctx_jit_info(fr_ctx* ctx, int* used, double* ms, int* compiled);
+/* *state = FR_JIT_* of the last render. For FR_JIT_FAILED, fr_last_error() then holds the
+   compiler's message. */
+int fr_ctx_jit_state(fr_ctx* ctx, int* state);
+/* Block until no scene-kernel compile is queued or running in this process. */
+int fr_jit_wait(void);
 
 /* ---- persistent multi-device context (tracer.rs:83-134 render_mt, one device per shard) ----
    Entry i of `devices` renders row shard i of n of every frame on its own fr_ctx (device

@@ -9,6 +9,14 @@
  *   abi_consumer render SCENE W H SPP DEPTH OUT
  *                                    render a scene file through fr_ctx_* on device 0 and
  *                                    write the f32 means, the u8 image and the stats to OUT
+ *   abi_consumer mrender SCENE W H SPP DEPTH OUT DEVICES
+ *                                    INTEGRATION.md's create_model / save_image sequence:
+ *                                    fr_mctx_create(DEVICES, e.g. "0,0"), two frames of
+ *                                    fr_mctx_render (FR_FLAG_WRITE_U8 | FR_FLAG_SCENE_JIT)
+ *                                    + fr_mctx_sync + fr_mctx_frame (the second after
+ *                                    fr_jit_wait, so it runs the scene kernel), fr_mctx_free;
+ *                                    both frames, their stats and every shard's
+ *                                    fr_ctx_jit_state go to OUT
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -89,7 +97,7 @@ static int fail(const char* what, int rc) {
   return 1;
 }
 
-static int render(const char* scene_path, uint32_t w, uint32_t h, uint32_t spp, uint32_t depth, const char* out) {
+static int load_scene(const char* scene_path, uint32_t w, uint32_t h, fr_scene** scene, fr_camera* cam) {
   FILE* f = fopen(scene_path, "rb");
   if (!f) return fail("fopen scene", -1);
   fseek(f, 0, SEEK_END);
@@ -98,11 +106,16 @@ static int render(const char* scene_path, uint32_t w, uint32_t h, uint32_t spp, 
   char* text = malloc((size_t)len);
   if (!text || fread(text, 1, (size_t)len, f) != (size_t)len) return fail("read scene", -1);
   fclose(f);
+  const int rc = fr_scene_from_json(text, (size_t)len, w, h, scene, cam);
+  free(text);
+  return rc ? fail("fr_scene_from_json", rc) : 0;
+}
+
+static int render(const char* scene_path, uint32_t w, uint32_t h, uint32_t spp, uint32_t depth, const char* out) {
   fr_scene* scene = NULL;
   fr_camera cam;
-  int rc = fr_scene_from_json(text, (size_t)len, w, h, &scene, &cam);
-  free(text);
-  if (rc) return fail("fr_scene_from_json", rc);
+  int rc = load_scene(scene_path, w, h, &scene, &cam);
+  if (rc) return rc;
   fr_params p;
   memset(&p, 0, sizeof(p));
   p.width = w;
@@ -141,11 +154,70 @@ static int render(const char* scene_path, uint32_t w, uint32_t h, uint32_t spp, 
   return 0;
 }
 
+/* The Rust binding's model (INTEGRATION.md create_model / frame / save_image / Drop) */
+static int mrender(const char* scene_path, uint32_t w, uint32_t h, uint32_t spp, uint32_t depth, const char* out,
+                   const char* devices_csv) {
+  int devices[64];
+  int n = 0;
+  for (const char* c = devices_csv; *c && n < 64;) {
+    devices[n++] = atoi(c);
+    while (*c && *c != ',') ++c;
+    if (*c == ',') ++c;
+  }
+  fr_scene* scene = NULL;
+  fr_camera cam;
+  int rc = load_scene(scene_path, w, h, &scene, &cam);
+  if (rc) return rc;
+  fr_mctx* mctx = NULL;
+  if ((rc = fr_mctx_create(devices, n, &mctx))) return fail("fr_mctx_create", rc);
+  fr_params p;
+  memset(&p, 0, sizeof(p));
+  p.width = w;
+  p.height = h;
+  p.spp = spp;
+  p.max_depth = depth;
+  p.seed = 0x5EED;
+  p.strip_rows = 8;
+  p.shard_index = 0; /* set per device by fr_mctx */
+  p.shard_count = 1;
+  p.flags = FR_FLAG_WRITE_U8 | FR_FLAG_SCENE_JIT;
+  FILE* o = fopen(out, "wb");
+  if (!o) return fail("fopen out", -1);
+  const size_t npx = (size_t)w * h * 3;
+  for (int frame = 0; frame < 2; ++frame) {
+    if (frame == 1 && (rc = fr_jit_wait())) return fail("fr_jit_wait", rc);
+    fr_stats st;
+    const float* mean = NULL;
+    const uint8_t* rgb8 = NULL;
+    if ((rc = fr_mctx_render(mctx, scene, &cam, &p))) return fail("fr_mctx_render", rc);
+    if ((rc = fr_mctx_sync(mctx, &st))) return fail("fr_mctx_sync", rc);
+    if ((rc = fr_mctx_frame(mctx, &mean, &rgb8))) return fail("fr_mctx_frame", rc);
+    fwrite(mean, sizeof(float), npx, o);
+    fwrite(rgb8, 1, npx, o);
+    const uint64_t counters[4] = {st.segments, st.hits, st.samples, st.scatters};
+    fwrite(counters, sizeof(uint64_t), 4, o);
+    for (int i = 0; i < n; ++i) {
+      fr_ctx* ctx = NULL;
+      int32_t state = -1;
+      if ((rc = fr_mctx_ctx(mctx, i, &ctx)) || (rc = fr_ctx_jit_state(ctx, &state))) return fail("fr_ctx_jit_state", rc);
+      fwrite(&state, sizeof(state), 1, o);
+    }
+  }
+  fclose(o);
+  fr_mctx_free(mctx);
+  fr_scene_free(scene);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 2 && strcmp(argv[1], "layout") == 0) return layout();
+  if (argc == 9 && strcmp(argv[1], "mrender") == 0)
+    return mrender(argv[2], (uint32_t)atoi(argv[3]), (uint32_t)atoi(argv[4]), (uint32_t)atoi(argv[5]),
+                   (uint32_t)atoi(argv[6]), argv[7], argv[8]);
   if (argc == 8 && strcmp(argv[1], "render") == 0)
     return render(argv[2], (uint32_t)atoi(argv[3]), (uint32_t)atoi(argv[4]), (uint32_t)atoi(argv[5]),
                   (uint32_t)atoi(argv[6]), argv[7]);
-  fprintf(stderr, "usage: %s layout | render SCENE W H SPP DEPTH OUT\n", argv[0]);
+  fprintf(stderr, "usage: %s layout | render SCENE W H SPP DEPTH OUT | mrender SCENE W H SPP DEPTH OUT DEVICES\n",
+          argv[0]);
   return 2;
 }

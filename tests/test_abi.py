@@ -23,7 +23,7 @@ def test_every_declared_symbol_is_exported(fr):
 
 
 def test_abi_version_and_struct_sizes(fr):
-    assert fr.lib().fr_abi_version() == fr.FR_ABI_VERSION == 5
+    assert fr.lib().fr_abi_version() == fr.FR_ABI_VERSION == 6
     assert C.sizeof(fr.FrPrim) == 88
     assert C.sizeof(fr.FrCamera) == 26 * 4
     assert C.sizeof(fr.FrParams) == 40  # static_assert-ed in render.hip

@@ -60,3 +60,37 @@ def test_c_consumer_render_equals_ctypes_path(consumer, gpu, tmp_path):
     assert np.array_equal(mean.view(np.uint32), m2.view(np.uint32))
     assert np.array_equal(u8, u2)
     assert list(cnt) == [st["segments"], st["hits"], st["samples"], st["scatters"]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", ["0,0", "0"])
+def test_c_consumer_multi_device_model_equals_ctypes_path(consumer, gpu, tmp_path, devices):
+    """INTEGRATION.md's exact create_model / save_image sequence from C: fr_mctx_create over
+    DEVICES, fr_mctx_render with FR_FLAG_WRITE_U8 | FR_FLAG_SCENE_JIT, fr_mctx_sync,
+    fr_mctx_frame, fr_mctx_free (tracer.rs:19-28, 160-187). Both of its frames (the first
+    may run the compiled-in kernel while the scene kernel compiles; the second, after
+    fr_jit_wait, runs the scene kernel on every shard) equal the ctypes fr_ctx render bit for
+    bit, with the same counters."""
+    w, h, spp, depth = 72, 44, 5, 8  # H % 8 != 0: a partial last strip
+    out = tmp_path / "mframe.bin"
+    subprocess.run([consumer, "mrender", gpu.scene_path("scene_08"), str(w), str(h), str(spp), str(depth), str(out),
+                    devices], check=True, timeout=300)
+    raw = out.read_bytes()
+    n, nd = w * h * 3, len(devices.split(","))
+    sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
+    m2, u2, st = gpu.render(sc, sc.camera, w, h, spp, depth)
+    frame_bytes = 5 * n + 32 + 4 * nd
+    assert len(raw) == 2 * frame_bytes
+    for k in range(2):
+        o = k * frame_bytes
+        mean = np.frombuffer(raw, np.float32, n, offset=o).reshape(h, w, 3)
+        u8 = np.frombuffer(raw, np.uint8, n, offset=o + 4 * n).reshape(h, w, 3)
+        cnt = np.frombuffer(raw, np.uint64, 4, offset=o + 5 * n)
+        states = list(np.frombuffer(raw, np.int32, nd, offset=o + 5 * n + 32))
+        assert np.array_equal(mean.view(np.uint32), m2.view(np.uint32)), k
+        assert np.array_equal(u8, u2), k
+        assert list(cnt) == [st["segments"], st["hits"], st["samples"], st["scatters"]], k
+        if k == 1:
+            assert states == [gpu.FR_JIT_USED] * nd, states
+        else:
+            assert all(s in (gpu.FR_JIT_USED, gpu.FR_JIT_PENDING) for s in states), states

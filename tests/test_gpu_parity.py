@@ -382,7 +382,7 @@ def test_multi_device_api_with_one_device(gpu):
     assert np.array_equal(a, b) and np.array_equal(au, bu)
 
 
-@pytest.mark.parametrize("n,jit", [(2, False), (8, False), (2, True), (8, True)])
+@pytest.mark.parametrize("n,jit", [(2, False), (8, False), (2, "wait"), (8, "wait")])
 def test_multi_context_matches_one_device_bit_for_bit(gpu, n, jit):
     """fr_mctx (tracer.rs:83-134's row tiling, one context per shard) with every entry on
     device 0: the stitched frame equals the N = 1 render bit for bit, frame after frame, and
@@ -552,7 +552,7 @@ def test_streamed_frames_match_the_oracle(gpu, shard, pipe, monkeypatch):
     ctx.close()
 
 
-@pytest.mark.parametrize("jit,pipe", [(False, "1"), (True, "1"), (False, "2"), (True, "2")])
+@pytest.mark.parametrize("jit,pipe", [(False, "1"), ("wait", "1"), (False, "2"), ("wait", "2")])
 def test_pipelined_frames_of_different_seeds(gpu, jit, pipe, monkeypatch):
     """Five frames of different seeds enqueued back to back with the frame pipeline, each
     gathered into its own pinned frame: every gather holds its own frame (the two frame
@@ -674,7 +674,7 @@ def test_c3_headline_frame_in_full(gpu):
     §4.11)."""
     name, w, h, spp, depth = "scene_08", 1920, 1080, 256, 8
     sc = gpu.Scene.from_file(gpu.scene_path(name), w, h)
-    runs = [gpu.render(sc, sc.camera, w, h, spp, depth, scene_jit=jit) for jit in (False, True)]
+    runs = [gpu.render(sc, sc.camera, w, h, spp, depth, scene_jit=jit) for jit in (False, "wait")]
     assert runs[0][2]["samples"] == w * h * spp == 530841600
     prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path(name)).read())
     cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
@@ -695,7 +695,7 @@ def test_c2_on_row_subset(gpu):
     mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
     assert st["samples"] == w * h * spp
     # the scene-specialised kernel renders the same frame bit for bit
-    jm, ju, jst = gpu.render(sc, sc.camera, w, h, spp, depth, scene_jit=True)
+    jm, ju, jst = gpu.render(sc, sc.camera, w, h, spp, depth, scene_jit="wait")
     assert np.array_equal(jm.view(np.uint32), mean.view(np.uint32)) and np.array_equal(ju, u8)
     assert (jst["segments"], jst["hits"], jst["scatters"]) == (st["segments"], st["hits"], st["scatters"])
     prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path(name)).read())
@@ -958,8 +958,8 @@ def test_absorbed_paths_skip_unwind_only_when_exact(gpu, colors):
 
 
 @pytest.mark.parametrize("pipe,buf_gb,jit", [("1", None, False), ("2", None, False), ("3", None, False),
-                                            ("5", None, False), ("2", "0.0002", False), ("3", None, True),
-                                            ("2", "0.0002", True)])
+                                            ("5", None, False), ("2", "0.0002", False), ("3", None, "wait"),
+                                            ("2", "0.0002", "wait")])
 def test_pass_pipeline_never_changes_results(gpu, pipe, buf_gb, jit, monkeypatch):
     """Passes on alternating streams with a double-buffered sample buffer (and, with a
     tiny FR_SAMPLE_BUFFER_GB, many passes reusing the two slots) give the same bits; jit:

@@ -1,0 +1,123 @@
+"""Host sanitizer build: the product's JSON parser, scene builder and BVH
+builder (fo-rma_amd/csrc/json_min.cpp, scene.cpp, bvh.cpp) and the oracle (oracle/oracle.cpp)
+compiled with -fsanitize=address,undefined -fno-sanitize-recover=all into one CPU program
+(tests/c/host_sanitize.cpp), then driven over every bundled scene, the generator's 10k-sphere
+scene (BASELINE config C5), a malformed-JSON corpus and a 150k-sphere BVH build. Any
+out-of-bounds access, use-after-free, leak or undefined behaviour aborts the program; every
+malformed file must fail cleanly with FR_EPARSE (the reference unwrap()s and panics,
+basics/scene_loader.rs:3-7)."""
+import glob
+import json
+import os
+import random
+import subprocess
+
+import pytest
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+SCENES = sorted(glob.glob(os.path.join(ROOT, "fo-rma_amd", "scenes", "*.min.json")))
+FR_OK, FR_EARG, FR_EPARSE = 0, -1, -2
+
+
+@pytest.fixture(scope="module")
+def exe(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("asan") / "host_sanitize")
+    srcs = [os.path.join(ROOT, "tests", "c", "host_sanitize.cpp")] + [
+        os.path.join(ROOT, "fo-rma_amd", "csrc", f) for f in ("json_min.cpp", "scene.cpp", "bvh.cpp")] + [
+        os.path.join(ROOT, "oracle", "oracle.cpp")]
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-fno-omit-frame-pointer", "-ffp-contract=off", "-fno-fast-math", "-pthread",
+                    "-I", os.path.join(ROOT, "include"), *srcs, "-o", out], check=True, timeout=600)
+    return out
+
+
+def _run(exe, *args):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    p = subprocess.run([exe, *args], capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
+    assert "Sanitizer" not in p.stderr and "runtime error" not in p.stderr, p.stderr[-4000:]
+    return [json.loads(line) for line in p.stdout.splitlines() if line.strip()]
+
+
+def _malformed_corpus(dirpath):
+    """Truncations, byte flips and hand-made bad documents around the bundled scenes."""
+    base = open(os.path.join(ROOT, "fo-rma_amd", "scenes", "scene_01.min.json"), "rb").read()
+    small = open(os.path.join(ROOT, "fo-rma_amd", "scenes", "scene_08.min.json"), "rb").read()
+    docs = {}
+    for k, cut in enumerate(sorted({1, 2, 10, 57, 200, len(base) // 3, len(base) // 2, len(base) - 2, len(base) - 1})):
+        docs[f"trunc_{k}"] = base[:cut]
+    rng = random.Random(5)
+    for k in range(40):
+        b = bytearray(small)
+        for _ in range(1 + k % 4):
+            b[rng.randrange(len(b))] = rng.choice(b'{}[],:"0-.eE+ \\tx\x00\xff')
+        docs[f"flip_{k}"] = bytes(b)
+    hand = {
+        "empty": b"",
+        "null": b"null",
+        "number": b"42",
+        "deep": b"[" * 300 + b"]" * 300,
+        "deep_obj": b'{"a":' * 300 + b"1" + b"}" * 300,
+        "huge_number": b'{"camera":{"position":[1e999,0,0],"rotation":[0,0,0,1],"fov":60},"objects":[]}',
+        "bad_escape": b'{"camera":{"position":[0,0,0],"rotation":[0,0,0,1],"fov":60},"objects":[{"mesh":"\\uZZZZ"}]}',
+        "string_pos": b'{"camera":{"position":"x","rotation":[0,0,0,1],"fov":60},"objects":[]}',
+        "short_vec": b'{"camera":{"position":[0,0],"rotation":[0,0,0,1],"fov":60},"objects":[]}',
+        "obj_not_list": b'{"camera":{"position":[0,0,0],"rotation":[0,0,0,1],"fov":60},"objects":7}',
+        "missing_camera": b'{"objects":[]}',
+        "unterminated": b'{"camera":{"position":[0,0,0',
+        "trailing": small + b"}}}",
+        "nul_inside": small[:40] + b"\x00" + small[41:],
+        "long_string": b'{"camera":{"position":[0,0,0],"rotation":[0,0,0,1],"fov":60},"objects":[{"mesh":"'
+                       + b"q" * 100000 + b'"}]}',
+        "many_objects_bad_tail": b'{"camera":{"position":[0,0,0],"rotation":[0,0,0,1],"fov":60},"objects":['
+                                 + b'{"mesh":"sphere","position":[0,0,0],"rotation":[0,0,0,1],"scale":[1,1,1]},' * 500
+                                 + b"]",
+    }
+    docs.update(hand)
+    paths = []
+    for name, data in docs.items():
+        p = os.path.join(dirpath, f"{name}.json")
+        with open(p, "wb") as f:
+            f.write(data)
+        paths.append(p)
+    return paths
+
+
+def test_bundled_scenes_load_clean_and_match_the_product_library(exe, fr):
+    res = _run(exe, "json", *SCENES)
+    assert [r["rc"] for r in res] == [FR_OK] * len(SCENES)
+    for r, path in zip(res, SCENES):
+        assert r["prims"] == len(fr.Scene.from_file(path, 32, 18)), path  # the product library's own build
+        assert r["oracle_rows"] == 18
+
+
+def test_generator_scene_bvh_build_clean(exe, tmp_path):
+    """BASELINE config C5's scene: tools/gen_scene.py's 10k spheres through the loader and the
+    BVH builder (and a tiny oracle render over the brute-force list)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_scene", os.path.join(ROOT, "tools", "gen_scene.py"))
+    gs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gs)
+    p = tmp_path / "gen10k.json"
+    p.write_text(gs.dumps(gs.generator_scene(10000, "sphere")))
+    (r,) = _run(exe, "json", str(p))
+    assert r["rc"] == FR_OK and r["prims"] == 10000
+    assert r["bvh"]["ok"] == 1 and r["bvh"]["order"] == 10000
+
+
+def test_malformed_json_corpus_fails_cleanly(exe, tmp_path):
+    paths = _malformed_corpus(str(tmp_path))
+    res = _run(exe, "json", *paths)
+    assert len(res) == len(paths)
+    by = {os.path.basename(r["file"])[:-5]: r for r in res}
+    for name in ("empty", "null", "number", "deep", "deep_obj", "unterminated", "trailing", "string_pos",
+                 "short_vec", "obj_not_list", "many_objects_bad_tail", "bad_escape"):
+        assert by[name]["rc"] == FR_EPARSE, (name, by[name])
+    for r in res:
+        assert r["rc"] in (FR_OK, FR_EPARSE), r
+
+
+def test_150k_sphere_bvh_build_clean(exe):
+    (r,) = _run(exe, "spheres", "150000")
+    assert r["rc"] == FR_OK and r["bvh"]["ok"] == 1 and r["bvh"]["order"] == 150000
