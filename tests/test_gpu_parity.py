@@ -687,27 +687,60 @@ def test_c3_headline_frame_in_full(gpu):
 
 
 @pytest.mark.slow
-def test_c2_on_row_subset(gpu):
-    """C2 (scene_01: 43 primitives with a plane, 1920x1080, 64 spp, 8 bounces): every 33rd
-    row (33 of 1,080 rows, all 1,920 pixels each) compared with the oracle."""
-    name, w, h, spp, depth, step = "scene_01", 1920, 1080, 64, 8, 33
+def test_c2_full_frame(gpu):
+    """C2 (scene_01: 43 primitives with a plane, 1920x1080, 64 spp, 8 bounces), the whole
+    frame against the oracle: all 2,073,600 pixels (132.7 M samples) within 1e-5 and bit for
+    bit, u8 identical, the whole-frame segment, hit and scatter counters equal. Both trace
+    kernels: the compiled-in one and the scene-specialised one."""
+    name, w, h, spp, depth = "scene_01", 1920, 1080, 64, 8
     sc = gpu.Scene.from_file(gpu.scene_path(name), w, h)
     mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, depth)
-    assert st["samples"] == w * h * spp
-    # the scene-specialised kernel (DESIGN.md §4.11) renders the same frame bit for bit
+    assert st["samples"] == w * h * spp == 132710400
     jm, ju, jst = gpu.render(sc, sc.camera, w, h, spp, depth, scene_jit="wait")
     assert np.array_equal(jm.view(np.uint32), mean.view(np.uint32)) and np.array_equal(ju, u8)
     assert (jst["segments"], jst["hits"], jst["scatters"]) == (st["segments"], st["hits"], st["scatters"])
     prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path(name)).read())
     cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
-    omean, ou8, ocnt, n = O.render(prims, cam, w, h, spp, depth, row_step=step, threads=oracle_threads())
-    rows = _rows(h, step)
-    assert n == len(rows) == 33
-    assert_parity(mean, u8, st, omean, ou8, None, rows=rows)
-    # size-independent properties of the whole frame
-    assert np.isfinite(mean).all() and (mean >= 0).all() and (mean <= 1).all()
-    assert st["hits"] <= st["segments"] <= st["samples"] * (depth + 1)
-    assert st["scatters"] <= st["hits"]
+    omean, ou8, ocnt = O.render_rows(prims, cam, w, h, spp, depth, range(h), threads=oracle_threads(), chunk=60,
+                                     progress=_progress("C2"))
+    assert ocnt["samples"] == st["samples"]
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
+
+
+@pytest.mark.slow
+def test_c4_full_frame_every_shard_through_mctx(gpu, monkeypatch):
+    """C4 (scene_08 3840x2160, 1024 spp, 8 bounces, row-tiled across 8 devices) as the
+    drop-in renders it: one fr_mctx over 8 contexts (here all on device 0), the scene kernel,
+    the whole 8.49 G-sample frame stitched in the page-locked host frame. Every shard is
+    checked: 4 full 3,840-px rows of each against the oracle (spread over the shard's
+    strips), and the stitched frame's counters equal the sum of the eight shard renders'."""
+    monkeypatch.setenv("FR_SAMPLE_BUFFER_GB", "12")  # one pass per shard, no frame slots: 8 x 8.5 GB
+    w, h, spp, depth, n = 3840, 2160, 1024, 8, 8
+    sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
+    m = gpu.MultiContext([0] * n)
+    try:
+        m.render(sc, sc.camera, gpu.make_params(w, h, spp, depth, scene_jit="wait"))
+        tot = m.sync()
+        shard_st = [m.context(i).sync() for i in range(n)]
+        assert all(m.context(i).jit_state() == gpu.FR_JIT_USED for i in range(n))
+        mean, u8 = m.frame()
+    finally:
+        m.close()
+    assert tot["samples"] == w * h * spp == 8493465600
+    for k in ("segments", "hits", "scatters", "samples"):
+        assert tot[k] == sum(s[k] for s in shard_st), k
+    assert not np.isnan(mean).any() and (mean >= 0).all() and (mean <= 1).all()
+    rows = []
+    for k in range(n):
+        mine = [y for y in range(h) if (y // 8) % n == k]
+        rows += [mine[0], mine[len(mine) // 3], mine[(2 * len(mine)) // 3], mine[-1]]
+    prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path("scene_08")).read())
+    cam = O.camera_look(frm, at, vup, fov, 0.1, w, h)
+    omean, ou8, _ = O.render_rows(prims, cam, w, h, spp, depth, rows, threads=oracle_threads(), chunk=4,
+                                  progress=_progress("C4 all shards"))
+    assert_parity(mean, u8, None, omean, ou8, None, rows=rows)
+    assert np.array_equal(mean[rows].view(np.uint32), omean[rows].view(np.uint32))
 
 
 # ---- BVH (scenes of >= 48 primitives, <= 32 planes; DESIGN.md §4.8) -------------
