@@ -14,7 +14,9 @@
 //   2. the disk cache (FR_JIT_CACHE, default $XDG_CACHE_HOME/forma_rt or ~/.cache/forma_rt;
 //      "0" disables), keyed by a hash of the embedded sources, the hiprtc options, the
 //      hiprtc and HIP runtime versions, the defines, the kernel name, the records and the
-//      target. A file that fails to load is deleted and compiled again once;
+//      target. Each file carries its code object's size and hash, checked before the bytes
+//      reach the loader (which aborts on a damaged code object); a file that fails the
+//      check, or fails to load, is deleted and the kernel compiled again once;
 //   3. hiprtc: on the caller's thread when it waits (fr_ctx_prepare, FR_FLAG_SCENE_JIT_WAIT),
 //      else on one background worker thread while renders run the compiled-in kernel.
 // Bounds: at most kMaxModules loaded modules (least recently used unloaded first, after its
@@ -139,6 +141,57 @@ bool read_file(const std::string& path, std::vector<char>& out) {
   const bool ok = n > 0 && fread(out.data(), 1, out.size(), f) == out.size();
   fclose(f);
   return ok;
+}
+
+// A disk-cache file is a 32-B header — magic, format version, code size, a 128-bit hash of
+// the code — then the code object. The HIP loader does not reject a damaged code object: it
+// aborts the process (a truncated file did, on the GPU box). So nothing read from disk
+// reaches hipModuleLoadData unless its size and hash check out.
+constexpr char kCacheMagic[4] = {'F', 'R', 'J', 'C'};
+constexpr uint32_t kCacheFormat = 1;
+constexpr size_t kCacheHeader = 32;
+
+void code_hash(const char* p, size_t n, uint64_t h[2]) {
+  h[0] = fnv1a(p, n, 0xcbf29ce484222325ull);
+  h[1] = fnv1a(p, n, 0x84222325cbf29ce4ull ^ n);
+}
+
+std::vector<char> wrap_code(const std::vector<char>& code) {
+  std::vector<char> out(kCacheHeader + code.size());
+  const uint64_t size = code.size();
+  uint64_t h[2];
+  code_hash(code.data(), code.size(), h);
+  memcpy(out.data(), kCacheMagic, 4);
+  memcpy(out.data() + 4, &kCacheFormat, 4);
+  memcpy(out.data() + 8, &size, 8);
+  memcpy(out.data() + 16, h, 16);
+  if (!code.empty()) memcpy(out.data() + kCacheHeader, code.data(), code.size());
+  return out;
+}
+
+// The code object of a cache file, or false (a damaged or foreign file: removed).
+bool read_cached_code(const std::string& path, std::vector<char>& code) {
+  std::vector<char> raw;
+  if (!read_file(path, raw)) return false;
+  uint32_t fmt = 0;
+  uint64_t size = 0, h[2] = {0, 0}, want[2];
+  bool ok = raw.size() > kCacheHeader && memcmp(raw.data(), kCacheMagic, 4) == 0;
+  if (ok) {
+    memcpy(&fmt, raw.data() + 4, 4);
+    memcpy(&size, raw.data() + 8, 8);
+    memcpy(want, raw.data() + 16, 16);
+    ok = fmt == kCacheFormat && size == raw.size() - kCacheHeader;
+  }
+  if (ok) {
+    code_hash(raw.data() + kCacheHeader, static_cast<size_t>(size), h);
+    ok = h[0] == want[0] && h[1] == want[1];
+  }
+  if (!ok) {
+    unlink(path.c_str());
+    return false;
+  }
+  code.assign(raw.begin() + kCacheHeader, raw.end());
+  return true;
 }
 
 // The file appears under `path` only when every byte reached the disk: a failed write,
@@ -346,7 +399,8 @@ class Registry {
       std::vector<char> bytes;
       const int rc = compile_checked(j.arch, j.prelude, j.name_expr, j.mname, bytes);
       const std::string err = rc ? fr_last_error() : "";
-      if (rc == FR_OK && !j.path.empty() && write_file_atomic(j.path, bytes)) prune_disk(j.path.substr(0, j.path.rfind('/')));
+      if (rc == FR_OK && !j.path.empty() && write_file_atomic(j.path, wrap_code(bytes)))
+        prune_disk(j.path.substr(0, j.path.rfind('/')));
       lk.lock();
       finish(j.key, rc, std::move(bytes), err, false);
     }
@@ -451,13 +505,13 @@ int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* 
       ++R.compiling;
       lk.unlock();
       std::vector<char> bytes;
-      if (attempt == 0 && !path.empty() && read_file(path, bytes)) {
+      if (attempt == 0 && !path.empty() && read_cached_code(path, bytes)) {
         lk.lock();
         R.finish(key, FR_OK, std::move(bytes), "", true);
       } else if (wait) {
         const int rc = compile_checked(arch, prelude, spec.name_expr, mname, bytes);
         const std::string err = rc ? fr_last_error() : "";
-        if (rc == FR_OK && !path.empty() && write_file_atomic(path, bytes)) prune_disk(dir);
+        if (rc == FR_OK && !path.empty() && write_file_atomic(path, wrap_code(bytes))) prune_disk(dir);
         st.compiled = 1;
         lk.lock();
         R.finish(key, rc, std::move(bytes), err, false);
