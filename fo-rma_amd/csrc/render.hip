@@ -159,6 +159,11 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   const bool mt = (kp.flags & FR_FLAG_MT_BANDS) != 0;
   const bool mt_zero = mt && !(kp.band_h && y / kp.band_h < 4u);  // rows render_mt never fills stay 0
   V3 sum = (first || !valid) ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
+  // 8-B records: the red and green channels travel as one packed pair (v_pk_mul_f32 /
+  // v_pk_add_f32: each lane-component is the plain IEEE product or sum, operands in the same
+  // order), blue alone: two VALU instead of three per level and per add
+  f2 sxy = {sum.x, sum.y};
+  float sz = sum.z;
   const float fspp = static_cast<float>(kp.spp);
   const uint32_t per = WPS * kp.ks;  // floats per slot in the buffer
   // full 16-sample slots: block bl + 1's loads are issued before block bl is summed, so
@@ -202,12 +207,11 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
       const uint32_t n = min(kBlockSamples, kp.spp - (kp.b0 + bl) * kBlockSamples);
       const float* c = tile + t * kSumSlot;
       for (uint32_t j = 0; j < n; ++j, c += WPS) {
+#ifdef FR_SUM_SCALAR  // A/B: the three channels one by one
         if (WPS == 2) {
           // 8-B record: terminal, then a_7 ... a_0 from 4-bit entries (kNibbleUnit: 1)
           const uint32_t tb = __float_as_uint(c[0]), w = __float_as_uint(c[1]);
           V3 col = tb == kDeferAbsorbed ? V3{0.0f, 0.0f, 0.0f} : sky_from_t(c[0]);
-          // level k's entry at byte 16 x nibble k: odd levels are the high nibble of byte
-          // k / 2 of w, even levels the high nibble of byte k / 2 of w << 4
           const uint32_t w4 = w << 4;
 #pragma unroll
           for (int k = 7; k >= 0; --k) {
@@ -215,7 +219,34 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
             const float4 e = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(att16) + off);
             col = mul(V3{e.x, e.y, e.z}, col);
           }
-          sum = add(sum, col);
+          sxy = sxy + f2{col.x, col.y};
+          sz = sz + col.z;
+#else
+        if (WPS == 2) {
+          // 8-B record: terminal, then a_7 ... a_0 from 4-bit entries (kNibbleUnit: 1)
+          const uint32_t tb = __float_as_uint(c[0]), w = __float_as_uint(c[1]);
+          // sky_from_t (rt_core.h), the same products and sums: (1 - t) 1 + t (0.5, 0.7, 1)
+          const float tt = c[0], u = 1.0f - tt;
+          const f2 uu = {u, u}, ttt = {tt, tt};
+          f2 cxy = uu * f2{1.0f, 1.0f} + ttt * f2{0.5f, 0.7f};
+          float cz = u * 1.0f + tt * 1.0f;
+          if (tb == kDeferAbsorbed) {
+            cxy = f2{0.0f, 0.0f};
+            cz = 0.0f;
+          }
+          // level k's entry at byte 16 x nibble k: odd levels are the high nibble of byte
+          // k / 2 of w, even levels the high nibble of byte k / 2 of w << 4
+          const uint32_t w4 = w << 4;
+#pragma unroll
+          for (int k = 7; k >= 0; --k) {
+            const uint32_t off = (((k & 1) ? w : w4) >> (8 * (k >> 1))) & 0xF0u;
+            const float4 e = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(att16) + off);
+            cxy = f2{e.x, e.y} * cxy;  // mul(a_k, col)
+            cz = e.z * cz;
+          }
+          sxy = sxy + cxy;  // add(sum, col)
+          sz = sz + cz;
+#endif
         } else if (defer) {
           // the deferred unwind (kDeferUnit): terminal, then a_7 ... a_0 innermost first
           const uint32_t tb = __float_as_uint(c[0]), lo = __float_as_uint(c[1]), hi = __float_as_uint(c[2]);
@@ -235,6 +266,7 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
       }
     }
   }
+  if (WPS == 2) sum = V3{sxy.x, sxy.y, sz};
   if (!valid) return;
   if (mt_zero) {
     if (last) {
@@ -964,10 +996,14 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   ks.n_segs = use_bvh ? dc->n_segs : 0u;
   ks.reach = kBvhOriginReach * (dc->bvh_extent + 1.0f);
   ks.att_nonneg = dc->att_nonneg ? 1u : 0u;
-  KCam kc{cam->position[0], cam->position[1], cam->position[2], cam->lower_left[0], cam->lower_left[1],
-          cam->lower_left[2], cam->horizontal[0], cam->horizontal[1], cam->horizontal[2], cam->vertical[0],
-          cam->vertical[1], cam->vertical[2], cam->u[0], cam->u[1], cam->u[2], cam->v[0], cam->v[1], cam->v[2],
-          cam->lens_radius};
+  KCam kc;
+  kc.px = cam->position[0], kc.py = cam->position[1], kc.pz = cam->position[2];
+  kc.lx = cam->lower_left[0], kc.ly = cam->lower_left[1], kc.lz = cam->lower_left[2];
+  kc.hx = cam->horizontal[0], kc.hy = cam->horizontal[1], kc.hz = cam->horizontal[2];
+  kc.vx = cam->vertical[0], kc.vy = cam->vertical[1], kc.vz = cam->vertical[2];
+  kc.ux = cam->u[0], kc.uy = cam->u[1], kc.uz = cam->u[2];
+  kc.bx = cam->v[0], kc.by = cam->v[1], kc.bz = cam->v[2];
+  kc.lens = cam->lens_radius;
   KParams kp;
   kp.W = p->width;
   kp.H = p->height;

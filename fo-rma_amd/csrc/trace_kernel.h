@@ -187,9 +187,12 @@ struct KWork {
 
 // camera.rs fields the ray generator reads: position, lower_left_corner,
 // horizontal, vertical, u, v (named b* here), lens_radius
+// Field order: the x, y pairs first (each pair 8-B aligned, so a pair of scalar registers
+// feeds a packed f32 operation), then the z components, then lens_radius.
 struct KCam {
-  float px, py, pz, lx, ly, lz, hx, hy, hz, vx, vy, vz, ux, uy, uz, bx, by, bz, lens;
+  float px, py, lx, ly, hx, hy, vx, vy, ux, uy, bx, by, pz, lz, hz, vz, uz, bz, lens;
 };
+static_assert(sizeof(KCam) == 19 * 4, "KCam is 19 floats");
 
 struct KArgs {
   KScene sc;
@@ -199,6 +202,9 @@ struct KArgs {
 };
 
 __device__ __forceinline__ V3 xyz(float4 a) { return V3{a.x, a.y, a.z}; }
+// a packed f32 pair: two components in one v_pk_add_f32 / v_pk_mul_f32 (each the plain IEEE
+// sum or product; sum_kernel's level products)
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 // The scene is read-only for the kernel's lifetime: reading it through the constant
 // address space lets the compiler use scalar loads even though the kernel stores to

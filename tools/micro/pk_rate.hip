@@ -30,6 +30,18 @@ __global__ __launch_bounds__(256) void rate(float* out, int iters) {
     } else if constexpr (KIND == 4) {  // 16 v_xor_b32
 #define X(x) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "v"(m));
       X(a0) X(a1) X(a2) X(a3) X(a4) X(a5) X(a6) X(a7) X(b0) X(b1) X(b2) X(b3) X(b4) X(b5) X(b6) X(b7)
+    } else if constexpr (KIND == 6) {  // 16 v_mul_f32 with an SGPR operand
+#define MS(x) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x) : "s"(m));
+      MS(a0) MS(a1) MS(a2) MS(a3) MS(a4) MS(a5) MS(a6) MS(a7) MS(b0) MS(b1) MS(b2) MS(b3) MS(b4) MS(b5) MS(b6) MS(b7)
+    } else if constexpr (KIND == 7) {  // 16 v_pk_mul_f32 with an SGPR-pair operand
+#define PS(x) asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(x) : "s"(mm));
+      PS(p0) PS(p1) PS(p2) PS(p3) PS(p4) PS(p5) PS(p6) PS(p7) PS(p0) PS(p1) PS(p2) PS(p3) PS(p4) PS(p5) PS(p6) PS(p7)
+    } else if constexpr (KIND == 8) {  // 16 v_add_f32 with an SGPR operand
+#define AS(x) asm volatile("v_add_f32 %0, %1, %0" : "+v"(x) : "s"(m));
+      AS(a0) AS(a1) AS(a2) AS(a3) AS(a4) AS(a5) AS(a6) AS(a7) AS(b0) AS(b1) AS(b2) AS(b3) AS(b4) AS(b5) AS(b6) AS(b7)
+    } else if constexpr (KIND == 9) {  // 16 v_mov_b32
+#define MV(x) asm volatile("v_mov_b32 %0, %0" : "+v"(x));
+      MV(a0) MV(a1) MV(a2) MV(a3) MV(a4) MV(a5) MV(a6) MV(a7) MV(b0) MV(b1) MV(b2) MV(b3) MV(b4) MV(b5) MV(b6) MV(b7)
     } else if constexpr (KIND == 5) {  // 16 v_max3_f32
 #define X3(x, y) asm volatile("v_max3_f32 %0, %0, %1, %1" : "+v"(x) : "v"(y));
       X3(a0, m) X3(a1, m) X3(a2, m) X3(a3, m) X3(a4, m) X3(a5, m) X3(a6, m) X3(a7, m) X3(b0, m) X3(b1, m) X3(b2, m)
@@ -48,11 +60,12 @@ int main() {
   hipGetDeviceProperties(&prop, 0);
   const int cus = prop.multiProcessorCount;
   const double ghz = prop.clockRate / 1e6;
-  const char* names[] = {"v_mul_f32", "v_pk_mul_f32", "v_pk_add_f32", "v_fma_f32", "v_xor_b32", "v_max3_f32"};
+  const char* names[] = {"v_mul_f32", "v_pk_mul_f32", "v_pk_add_f32", "v_fma_f32", "v_xor_b32", "v_max3_f32",
+                         "v_mul_f32 (sgpr)", "v_pk_mul_f32 (sgpr pair)", "v_add_f32 (sgpr)", "v_mov_b32"};
   const int iters = 20000;
-  for (int waves_per_simd = 1; waves_per_simd <= 8; waves_per_simd *= 2) {
+  for (int waves_per_simd = 4; waves_per_simd <= 8; waves_per_simd *= 2) {
     const int blocks = cus * waves_per_simd;  // 256 threads = 4 waves = one per SIMD
-    for (int k = 0; k < 6; ++k) {
+    for (int k = 0; k < 10; ++k) {
       hipEvent_t e0, e1;
       hipEventCreate(&e0);
       hipEventCreate(&e1);
@@ -64,6 +77,10 @@ int main() {
           case 3: hipLaunchKernelGGL(rate<3>, dim3(blocks), dim3(256), 0, 0, d, iters); break;
           case 4: hipLaunchKernelGGL(rate<4>, dim3(blocks), dim3(256), 0, 0, d, iters); break;
           case 5: hipLaunchKernelGGL(rate<5>, dim3(blocks), dim3(256), 0, 0, d, iters); break;
+          case 6: hipLaunchKernelGGL(rate<6>, dim3(blocks), dim3(256), 0, 0, d, iters); break;
+          case 7: hipLaunchKernelGGL(rate<7>, dim3(blocks), dim3(256), 0, 0, d, iters); break;
+          case 8: hipLaunchKernelGGL(rate<8>, dim3(blocks), dim3(256), 0, 0, d, iters); break;
+          case 9: hipLaunchKernelGGL(rate<9>, dim3(blocks), dim3(256), 0, 0, d, iters); break;
         }
       };
       launch();
