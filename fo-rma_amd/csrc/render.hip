@@ -159,11 +159,6 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   const bool mt = (kp.flags & FR_FLAG_MT_BANDS) != 0;
   const bool mt_zero = mt && !(kp.band_h && y / kp.band_h < 4u);  // rows render_mt never fills stay 0
   V3 sum = (first || !valid) ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
-  // 8-B records: the red and green channels travel as one packed pair (v_pk_mul_f32 /
-  // v_pk_add_f32: each lane-component is the plain IEEE product or sum, operands in the same
-  // order), blue alone: two VALU instead of three per level and per add
-  f2 sxy = {sum.x, sum.y};
-  float sz = sum.z;
   const float fspp = static_cast<float>(kp.spp);
   const uint32_t per = WPS * kp.ks;  // floats per slot in the buffer
   // full 16-sample slots: block bl + 1's loads are issued before block bl is summed, so
@@ -207,33 +202,10 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
       const uint32_t n = min(kBlockSamples, kp.spp - (kp.b0 + bl) * kBlockSamples);
       const float* c = tile + t * kSumSlot;
       for (uint32_t j = 0; j < n; ++j, c += WPS) {
-#ifdef FR_SUM_SCALAR  // A/B: the three channels one by one
         if (WPS == 2) {
           // 8-B record: terminal, then a_7 ... a_0 from 4-bit entries (kNibbleUnit: 1)
           const uint32_t tb = __float_as_uint(c[0]), w = __float_as_uint(c[1]);
           V3 col = tb == kDeferAbsorbed ? V3{0.0f, 0.0f, 0.0f} : sky_from_t(c[0]);
-          const uint32_t w4 = w << 4;
-#pragma unroll
-          for (int k = 7; k >= 0; --k) {
-            const uint32_t off = (((k & 1) ? w : w4) >> (8 * (k >> 1))) & 0xF0u;
-            const float4 e = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(att16) + off);
-            col = mul(V3{e.x, e.y, e.z}, col);
-          }
-          sxy = sxy + f2{col.x, col.y};
-          sz = sz + col.z;
-#else
-        if (WPS == 2) {
-          // 8-B record: terminal, then a_7 ... a_0 from 4-bit entries (kNibbleUnit: 1)
-          const uint32_t tb = __float_as_uint(c[0]), w = __float_as_uint(c[1]);
-          // sky_from_t (rt_core.h), the same products and sums: (1 - t) 1 + t (0.5, 0.7, 1)
-          const float tt = c[0], u = 1.0f - tt;
-          const f2 uu = {u, u}, ttt = {tt, tt};
-          f2 cxy = uu * f2{1.0f, 1.0f} + ttt * f2{0.5f, 0.7f};
-          float cz = u * 1.0f + tt * 1.0f;
-          if (tb == kDeferAbsorbed) {
-            cxy = f2{0.0f, 0.0f};
-            cz = 0.0f;
-          }
           // level k's entry at byte 16 x nibble k: odd levels are the high nibble of byte
           // k / 2 of w, even levels the high nibble of byte k / 2 of w << 4
           const uint32_t w4 = w << 4;
@@ -241,12 +213,9 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
           for (int k = 7; k >= 0; --k) {
             const uint32_t off = (((k & 1) ? w : w4) >> (8 * (k >> 1))) & 0xF0u;
             const float4 e = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(att16) + off);
-            cxy = f2{e.x, e.y} * cxy;  // mul(a_k, col)
-            cz = e.z * cz;
+            col = mul(V3{e.x, e.y, e.z}, col);
           }
-          sxy = sxy + cxy;  // add(sum, col)
-          sz = sz + cz;
-#endif
+          sum = add(sum, col);
         } else if (defer) {
           // the deferred unwind (kDeferUnit): terminal, then a_7 ... a_0 innermost first
           const uint32_t tb = __float_as_uint(c[0]), lo = __float_as_uint(c[1]), hi = __float_as_uint(c[2]);
@@ -266,7 +235,6 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
       }
     }
   }
-  if (WPS == 2) sum = V3{sxy.x, sxy.y, sz};
   if (!valid) return;
   if (mt_zero) {
     if (last) {
@@ -692,6 +660,9 @@ static std::string jit_defines() {
   def("FR_FINE_SAMPLES", FR_FINE_SAMPLES);
   def("FR_STAGE", FR_STAGE);
   def("FR_BVH_STAGE", FR_BVH_STAGE);
+#ifdef FR_TRACE_PRIO
+  def("FR_TRACE_PRIO", FR_TRACE_PRIO);
+#endif
 #ifdef FR_MIN_WAVES
   def("FR_MIN_WAVES", FR_MIN_WAVES);
 #else

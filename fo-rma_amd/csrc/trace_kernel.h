@@ -187,10 +187,8 @@ struct KWork {
 
 // camera.rs fields the ray generator reads: position, lower_left_corner,
 // horizontal, vertical, u, v (named b* here), lens_radius
-// Field order: the x, y pairs first (each pair 8-B aligned, so a pair of scalar registers
-// feeds a packed f32 operation), then the z components, then lens_radius.
 struct KCam {
-  float px, py, lx, ly, hx, hy, vx, vy, ux, uy, bx, by, pz, lz, hz, vz, uz, bz, lens;
+  float px, py, pz, lx, ly, lz, hx, hy, hz, vx, vy, vz, ux, uy, uz, bx, by, bz, lens;
 };
 static_assert(sizeof(KCam) == 19 * 4, "KCam is 19 floats");
 
@@ -202,9 +200,6 @@ struct KArgs {
 };
 
 __device__ __forceinline__ V3 xyz(float4 a) { return V3{a.x, a.y, a.z}; }
-// a packed f32 pair: two components in one v_pk_add_f32 / v_pk_mul_f32 (each the plain IEEE
-// sum or product; sum_kernel's level products)
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 // The scene is read-only for the kernel's lifetime: reading it through the constant
 // address space lets the compiler use scalar loads even though the kernel stores to
@@ -425,6 +420,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // Entry n of the attenuations is (1, 1, 1): the depth-8 stack's empty levels hold n.
   // Staging the winner's data keeps per-lane global gathers off the shading path.
   // [STG > 1: kBlock x STG staged sample colours (12 B each), lane-major] in front.
+#ifndef FR_TRACE_PRIO
+#define FR_TRACE_PRIO 0
+#endif
+  // FR_TRACE_PRIO (A/B): the trace's waves issue ahead of a concurrently running sum_kernel
+  // (the frame pipeline), which then only takes the issue slots the trace
+  // leaves idle
+  if (FR_TRACE_PRIO) __builtin_amdgcn_s_setprio(FR_TRACE_PRIO);
   extern __shared__ uint32_t lds[];
   constexpr uint32_t STG = stage_samples(BVH);
   constexpr bool NIB = DEFER == 2;             // 8-B records, winners in a register
