@@ -216,6 +216,24 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
             col = mul(V3{e.x, e.y, e.z}, col);
           }
           sum = add(sum, col);
+        } else if (kSkyDefer && (kp.flags & KF_NIBBLE)) {
+          // FR_SKY_DEFER's 12-B record {d.y, dot(d, d), winners}: the sky parameter here
+          const float dd = c[1];
+          const uint32_t w = __float_as_uint(c[2]);
+#ifdef FR_SKY_SUM_IEEE
+          const float tt = sky_t_from(c[0], dd);
+#else
+          const float tt = sky_t_fast_from(c[0], dd);  // bit-identical (fr_selftest_ops op 14)
+#endif
+          V3 col = __float_as_uint(dd) == kDeferAbsorbed ? V3{0.0f, 0.0f, 0.0f} : sky_from_t(tt);
+          const uint32_t w4 = w << 4;
+#pragma unroll
+          for (int k = 7; k >= 0; --k) {
+            const uint32_t off = (((k & 1) ? w : w4) >> (8 * (k >> 1))) & 0xF0u;
+            const float4 e = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(att16) + off);
+            col = mul(V3{e.x, e.y, e.z}, col);
+          }
+          sum = add(sum, col);
         } else if (defer) {
           // the deferred unwind (kDeferUnit): terminal, then a_7 ... a_0 innermost first
           const uint32_t tb = __float_as_uint(c[0]), lo = __float_as_uint(c[1]), hi = __float_as_uint(c[2]);
@@ -663,6 +681,9 @@ static std::string jit_defines() {
 #ifdef FR_TRACE_PRIO
   def("FR_TRACE_PRIO", FR_TRACE_PRIO);
 #endif
+#ifdef FR_SKY_DEFER
+  d += "#define FR_SKY_DEFER\n";
+#endif
 #ifdef FR_MIN_WAVES
   def("FR_MIN_WAVES", FR_MIN_WAVES);
 #else
@@ -1016,7 +1037,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   // FR_MAT=0 keeps the general shading step for diffuse-only scenes (A/B, tests)
   const char* mat_env = getenv("FR_MAT");
   if (dc->diffuse && !(mat_env && strcmp(mat_env, "0") == 0)) kp.flags |= KF_DIFFUSE;
-  const uint32_t wps = nibble ? 2u : 3u;  // words per sample in the buffer
+  const uint32_t wps = nibble && !kSkyDefer ? 2u : 3u;  // words per sample in the buffer
   const size_t per_block = static_cast<size_t>(kp.P) * kp.ks * wps * sizeof(float);
   uint32_t want_passes = 1;
   if (const char* e = getenv("FR_PIPELINE")) want_passes = static_cast<uint32_t>(atoi(e) > 0 ? atoi(e) : 1);
@@ -1226,7 +1247,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     }
     const int first = pass == 0, last = pass + 1 >= passes;
     if (first && c->copy_pending) HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_copy, 0));  // last gather done
-    hipLaunchKernelGGL(nibble ? sum_kernel<2> : sum_kernel<3>, dim3(sum_blocks ? sum_blocks : 1u), dim3(kSumThreads), 0,
+    hipLaunchKernelGGL(wps == 2 ? sum_kernel<2> : sum_kernel<3>, dim3(sum_blocks ? sum_blocks : 1u), dim3(kSumThreads), 0,
                        c->stream_sum, kp, samples,
                        c->d_running, c->d_mean, c->d_u8, first, last, ks.att, dc->n);
     HIPCHK(hipGetLastError());

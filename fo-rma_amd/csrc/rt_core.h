@@ -504,6 +504,9 @@ FR_HD float sky_t(V3 d) {
   const V3 ud = unit(d);
   return 0.5f * (ud.y + 1.0f);
 }
+// sky_t from the two values it depends on, d.y and dot(d, d) in length()'s order: the same
+// operations (a division by the correctly rounded sqrt, then the blend parameter)
+FR_HD float sky_t_from(float dy, float dd) { return 0.5f * (dy / sqrtf(dd) + 1.0f); }
 FR_HD V3 sky_from_t(float t) { return add(scl(1.0f - t, V3{1.0f, 1.0f, 1.0f}), scl(t, V3{0.5f, 0.7f, 1.0f})); }
 FR_HD V3 sky(V3 d) { return sky_from_t(sky_t(d)); }
 
@@ -516,9 +519,8 @@ FR_HD V3 sky(V3 d) { return sky_from_t(sky_t(d)); }
 // steps identities for |d.y| in {0} u [2^-100, 2^100]; a quotient below 2^-26, where the
 // core sequence could differ in the denormal range, gives 1 + q = 1 either way). Other
 // lanes take the plain expression. Bit-identical to sky_t: fr_selftest_ops op 14.
-__device__ __forceinline__ float sky_t_fast(V3 d) {
-  const float dd = d.x * d.x + d.y * d.y + d.z * d.z;  // length()'s sum, in its order
-  const float ay = __builtin_fabsf(d.y);
+__device__ __forceinline__ float sky_t_fast_from(float dy, float dd) {
+  const float ay = __builtin_fabsf(dy);
   const bool fast = (dd >= 0x1p-96f) & (dd <= 0x1p126f) & ((ay >= 0x1p-100f) | (ay == 0.0f));
   if (fast) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -529,11 +531,14 @@ __device__ __forceinline__ float sky_t_fast(V3 d) {
     const float rup = __builtin_fmaf(-sup, s, dd);
     float len = rdn <= 0.0f ? sdn : s;
     len = rup > 0.0f ? sup : len;
-    const float q = div_rn(d.y, len, recip_nr(len));
+    const float q = div_rn(dy, len, recip_nr(len));
     return 0.5f * (q + 1.0f);
 #endif
   }
-  return sky_t(d);
+  return sky_t_from(dy, dd);  // = sky_t(d): the same operations on the same values
+}
+__device__ __forceinline__ float sky_t_fast(V3 d) {
+  return sky_t_fast_from(d.y, d.x * d.x + d.y * d.y + d.z * d.z);  // length()'s sum, in its order
 }
 #endif
 

@@ -97,6 +97,15 @@ constexpr uint32_t kNibbleMaxPrims = 15;
 constexpr uint32_t kNibbleUnit = 15;
 constexpr uint32_t KF_NIBBLE = 1u << 29;           // internal: 8-B deferred records
 constexpr uint32_t KF_DIFFUSE = 1u << 28;          // internal: no metal/dielectric (trace_kernel MAT = 1)
+// FR_SKY_DEFER builds (A/B): the 8-B-record kernel stores 12-B records {d.y, dot(d, d),
+// winners} and sum_kernel computes the sky parameter, at full SIMD width, instead of the
+// trace kernel in the few lanes whose path escapes in a given iteration. dot(d, d) = -1
+// (which no sum of squares is) marks an absorbed path.
+#ifdef FR_SKY_DEFER
+constexpr bool kSkyDefer = true;
+#else
+constexpr bool kSkyDefer = false;
+#endif
 #ifndef FR_BLOCK_SAMPLES
 #define FR_BLOCK_SAMPLES 16  // RNG contract: one stream per 16-sample block (oracle.cpp agrees)
 #endif
@@ -431,7 +440,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   constexpr uint32_t STG = stage_samples(BVH);
   constexpr bool NIB = DEFER == 2;             // 8-B records, winners in a register
   constexpr bool DIFFUSE = MAT == 1;           // lambertian scatters only
-  constexpr uint32_t WPS = NIB ? 2u : 3u;      // words per sample in the buffer
+  constexpr bool SKYD = NIB && kSkyDefer;      // 12-B records {d.y, dot(d, d), winners}
+  constexpr uint32_t WPS = NIB && !SKYD ? 2u : 3u;  // words per sample in the buffer
   // list kernels always stage; BVH kernels when the launch gave them the LDS (KF_STAGE)
   const bool staged = STG > 1 && (!BVH || (kp.flags & KF_STAGE) != 0u);
   float* stage = reinterpret_cast<float*>(lds) + threadIdx.x * (WPS * STG);
@@ -688,7 +698,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     PROF_MARK(PF_CLAIM);
     bool ended = false;
     V3 term{0.0f, 0.0f, 0.0f};
-    uint32_t tsky = kDeferAbsorbed;  // DEFER: the terminal as sky parameter bits
+    uint32_t tsky = kDeferAbsorbed;  // DEFER: the terminal as sky parameter bits (SKYD: dot(d, d))
+    float sky_dy = 0.0f;             // SKYD: the escaping ray's d.y
     if (need != NEED_NONE) {
       // 1. merged rejection loop
       float px = 0.0f, py = 0.0f, pz = 0.0f;
@@ -1025,7 +1036,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       }
       PROF_MARK(PF_HIT);
       if (best < 0) {
-        if (DEFER)
+        if (SKYD) {
+          sky_dy = d.y;
+          tsky = __float_as_uint(d.x * d.x + d.y * d.y + d.z * d.z);  // length()'s sum, in its order
+        } else if (DEFER)
 #ifdef FR_FAST_SKY
           tsky = __float_as_uint(sky_t_fast(d));  // tracer.rs:211-218, the blend in sum_kernel
 #else
@@ -1113,7 +1127,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       DIAG_WAVE(DG_END_W);
       DIAG_LANE(DG_END_L);
       V3 col = term;
-      if (NIB) {
+      if (SKYD) {
+        col = V3{sky_dy, __uint_as_float(tsky), __uint_as_float(wnib)};
+        wnib = ~0u;  // the next sample starts empty
+      } else if (NIB) {
         col = V3{__uint_as_float(tsky), __uint_as_float(wnib), 0.0f};
         wnib = ~0u;  // the next sample starts empty
       } else if (DEFER) {
