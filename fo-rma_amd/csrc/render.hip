@@ -118,7 +118,11 @@ static uint32_t scatter_class(const fr_prim& p) {
 // KF_DEFER the slots hold deferred-unwind records (kDeferUnit) and the colour is rebuilt
 // here from a 12-B-per-entry attenuation table (tile + table fit three workgroups per CU).
 // WPS = 2: 8-B records {t, 4-bit winners} (KF_NIBBLE).
-constexpr uint32_t kSumThreads = 256;
+#ifndef FR_SUM_THREADS
+#define FR_SUM_THREADS 256  // 64 (A/B): one-wave workgroups, no barrier between the slot's waves
+#endif
+constexpr uint32_t kSumThreads = FR_SUM_THREADS;
+static_assert(kSumThreads % 64u == 0 && kSumThreads <= kDeferUnit + 1u, "whole waves, one table pass or more");
 
 template <uint32_t WPS>
 __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const float* __restrict__ samples,
@@ -145,12 +149,14 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   if (FR_SUM_PRIO) __builtin_amdgcn_s_setprio(FR_SUM_PRIO);
   const uint32_t t = threadIdx.x;
   const bool defer = (kp.flags & KF_DEFER) != 0;
-  if (defer) {  // kSumThreads == kDeferUnit + 1
-    const float4 a = t < n_prims ? att[t] : make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-    att_s[3 * t] = a.x;
-    att_s[3 * t + 1] = a.y;
-    att_s[3 * t + 2] = a.z;
-    if (t < 16u) att16[t] = make_float4(a.x, a.y, a.z, 0.0f);
+  if (defer) {  // the kDeferUnit + 1 table entries, kSumThreads at a time
+    for (uint32_t i = t; i <= kDeferUnit; i += kSumThreads) {
+      const float4 a = i < n_prims ? att[i] : make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+      att_s[3 * i] = a.x;
+      att_s[3 * i + 1] = a.y;
+      att_s[3 * i + 2] = a.z;
+      if (i < 16u) att16[i] = make_float4(a.x, a.y, a.z, 0.0f);
+    }
   }
   const uint32_t q0 = blockIdx.x * kSumThreads, q = q0 + t;
   const uint32_t nq = min(kSumThreads, kp.P - q0);
