@@ -545,8 +545,11 @@ def run_mctx(a, plan, torch, fr):
         c.trace_log(True)
     sync_all()
     t0 = time.perf_counter()
+    host_ms = 0.0  # host time inside fr_mctx_render (enqueueing every shard and gather)
     for _ in range(a.steps):
+        th = time.perf_counter()
         mc.render(scene, cam, params)
+        host_ms += (time.perf_counter() - th) * 1e3
         rendered[0] = True
         if a.sync_each:
             mc.sync()
@@ -587,6 +590,7 @@ def run_mctx(a, plan, torch, fr):
         "host_sync": "each step" if a.sync_each else "after the K steps (frames streamed back to back)",
         "segments_per_sample": round(total["segments"] / max(1, total["samples"]), 4),
         "scatters_per_sample": round(total["scatters"] / max(1, total["samples"]), 4),
+        "host_enqueue_ms_per_frame": round(host_ms / max(1, a.steps), 4),
         "trace_kernel_ms_per_launch_max_shard": slow["trace_ms_per_launch"],
         "trace_kernel_ms_per_launch_min_shard": min(s["trace_ms_per_launch"] for s in shards),
         "shards": shards,

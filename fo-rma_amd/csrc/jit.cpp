@@ -31,6 +31,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -325,6 +326,7 @@ struct Module {
   hipFunction_t fn = nullptr;
   int device = 0;
   uint64_t used = 0;
+  std::shared_ptr<void> pin = std::make_shared<char>(0);  // copies held by callers (JitStats::pin)
 };
 
 struct Job {  // a background compile: everything copied, nothing borrowed from the caller
@@ -437,8 +439,8 @@ const std::string& toolchain() {
 }
 
 // Unload a module evicted from the table once its device has drained: a launch of it may
-// still be queued on a stream (the evicted module is the least recently resolved one, so
-// no render is between resolving it and launching it).
+// still be queued on a stream. No caller holds it (unpinned): a render that looked it up
+// holds its pin from the lookup through the launch.
 void unload_evicted(const Module& m) {
   int cur = -1;
   (void)hipGetDevice(&cur);
@@ -494,6 +496,7 @@ int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* 
     mi->second.used = ++R.tick;
     *out = mi->second.fn;
     st.reused = 1;
+    st.pin = mi->second.pin;
     return done(FR_JIT_USED);
   }
   // attempt 0 may take the disk cache; a disk file that does not load is deleted and the
@@ -570,6 +573,7 @@ int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* 
       if (prev != R.modules.end()) {
         prev->second.used = ++R.tick;
         *out = prev->second.fn;
+        st.pin = prev->second.pin;
         return done(FR_JIT_USED);
       }
       continue;
@@ -577,14 +581,20 @@ int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* 
     m.used = ++R.tick;
     R.modules[mkey] = m;
     *out = m.fn;
+    st.pin = m.pin;
+    // evict the least recently used modules beyond the bound, among those no caller pins
+    // (a pin is copied only under this lock, so an unpinned module stays unpinned here)
     std::vector<Module> evicted;
     while (R.modules.size() > kMaxModules) {
-      auto victim = R.modules.begin();
+      auto victim = R.modules.end();
       for (auto v = R.modules.begin(); v != R.modules.end(); ++v)
-        if (v->second.used < victim->second.used) victim = v;
+        if (v->second.pin.use_count() == 1 && (victim == R.modules.end() || v->second.used < victim->second.used))
+          victim = v;
+      if (victim == R.modules.end()) break;  // every module is pinned: stay over the bound
       evicted.push_back(victim->second);
       R.modules.erase(victim);
     }
+
     lk.unlock();
     for (const Module& v : evicted) unload_evicted(v);
     return done(FR_JIT_USED);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <memory>
 #include <string>
 
 namespace fr {
@@ -28,6 +29,9 @@ struct JitStats {
   int reused = 0;    // 1: the module was already loaded in this process
   int state = 0;     // FR_JIT_* (forma_rt.h): USED, PENDING (no kernel yet) or FAILED
   std::string error; // FAILED: the compiler's message
+  // USED: holds the module loaded: while any copy of it lives, the LRU never unloads the
+  // module, so a caller may keep the function handle with it (fr_ctx's kernel cache)
+  std::shared_ptr<void> pin;
 };
 
 // The scene kernel for spec on `device` (the current device must be `device`).
@@ -43,6 +47,7 @@ int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* 
 
 // Block until the background worker has no compile queued or running.
 int jit_wait_all();
+
 
 // hiprtc only, no device (tests): compiles spec for arch and checks that the kernel's
 // lowered name is the one jit_trace_kernel looks up.
