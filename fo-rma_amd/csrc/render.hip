@@ -1250,7 +1250,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       // persistent grid: the resident workgroup count (launch_persistent)
       uint32_t blocks = 0;
       Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy, &blocks,
-                use_bvh && stage_n > 1 ? kBlock * stage_n * 3 * sizeof(float) : 0u};
+                use_bvh && stage_n > 1 && !FR_BVH_RSTAGE ? kBlock * stage_n * 3 * sizeof(float) : 0u};
       // pipelined frames leave room on every CU for the previous frame's sum workgroups
       if (fpipe) {
         const char* r = getenv("FR_FRAME_PIPE_RESERVE");

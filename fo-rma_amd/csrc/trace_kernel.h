@@ -253,6 +253,11 @@ constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for smal
 #define FR_BVH_STAGE 2
 #endif
 __host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? FR_BVH_STAGE : FR_STAGE; }
+// FR_BVH_RSTAGE=1: the BVH kernels hold a pair's first colour in registers instead of LDS
+// (3 VGPRs, none of the traversal stack's LDS), so every BVH launch stores whole pairs.
+#ifndef FR_BVH_RSTAGE
+#define FR_BVH_RSTAGE 0
+#endif
 // a sub-block starts on a staging group: the group's store covers only its own samples
 static_assert(kFineSamples % FR_STAGE == 0, "sub-blocks hold whole staging groups");
 
@@ -443,7 +448,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   constexpr bool SKYD = NIB && kSkyDefer;      // 12-B records {d.y, dot(d, d), winners}
   constexpr uint32_t WPS = NIB && !SKYD ? 2u : 3u;  // words per sample in the buffer
   // list kernels always stage; BVH kernels when the launch gave them the LDS (KF_STAGE)
-  const bool staged = STG > 1 && (!BVH || (kp.flags & KF_STAGE) != 0u);
+  constexpr bool RSTG = BVH && FR_BVH_RSTAGE != 0;  // pairs staged in registers
+  const bool staged = STG > 1 && !RSTG && (!BVH || (kp.flags & KF_STAGE) != 0u);
   float* stage = reinterpret_cast<float*>(lds) + threadIdx.x * (WPS * STG);
   // DEFER kernels (<= kDeferMaxPrims primitives) always hold the attenuations in LDS, and
   // the 8-B-record kernels (<= kNibbleMaxPrims) the records too: compile-time facts there,
@@ -518,6 +524,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   bool smetal = false;
   uint32_t sbest = 0, s = 0, s_end = 0, nseg = 0, nhit = 0, nscat = 0;
   uint32_t jj = 0;           // sample index within the item's block
+  V3 pend{0.0f, 0.0f, 0.0f};  // RSTG: the pair's first colour (an even jj)
 #ifdef FR_DIAG
   uint32_t diag_tb = 0, diag_seg0 = 0;  // the item's batch index, segments at its claim
   uint32_t diag_iter = 0;               // loop iterations of this wave
@@ -1172,7 +1179,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           for (int j = udepth - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
         }
       }
-      if (!staged) {
+      if (RSTG) {
+        // pairs start on even jj (blocks and sub-blocks do): the odd sample stores both
+        if (jj & 1u) {
+          float* dst = out + WPS * (jj - 1u);
+          if (kp.ks == kBlockSamples) {
+            if constexpr (WPS == 3u) {
+              // 8-B aligned: item * 192 B + a multiple of 24 B
+              reinterpret_cast<float2*>(dst)[0] = make_float2(pend.x, pend.y);
+              reinterpret_cast<float2*>(dst)[1] = make_float2(pend.z, col.x);
+              reinterpret_cast<float2*>(dst)[2] = make_float2(col.y, col.z);
+            } else {
+              // 16-B aligned: item * 128 B + a multiple of 16 B
+              *reinterpret_cast<float4*>(dst) = make_float4(pend.x, pend.y, col.x, col.y);
+            }
+          } else {
+            dst[0] = pend.x;
+            dst[1] = pend.y;
+            if (WPS == 3) dst[2] = pend.z;
+            dst[WPS] = col.x;
+            dst[WPS + 1] = col.y;
+            if (WPS == 3) dst[WPS + 2] = col.z;
+          }
+        } else if (s + 1u == s_end) {
+          out[WPS * jj] = col.x;
+          out[WPS * jj + 1] = col.y;
+          if (WPS == 3) out[WPS * jj + 2] = col.z;
+        } else {
+          pend = col;
+        }
+      } else if (!staged) {
         out[WPS * jj] = col.x;
         out[WPS * jj + 1] = col.y;
         if (WPS == 3) out[WPS * jj + 2] = col.z;
