@@ -124,6 +124,13 @@ static uint32_t scatter_class(const fr_prim& p) {
 #define FR_SUM_THREADS 256  // 64 (A/B): one-wave workgroups, no barrier between the slot's waves
 #endif
 constexpr uint32_t kSumThreads = FR_SUM_THREADS;
+#ifndef FR_SUM_UNROLL
+#define FR_SUM_UNROLL 2
+#endif
+constexpr int kSumUnroll = FR_SUM_UNROLL;
+#ifndef FR_SUM_SELECT
+#define FR_SUM_SELECT 0
+#endif
 static_assert(kSumThreads % 64u == 0 && kSumThreads <= kDeferUnit + 1u, "whole waves, one table pass or more");
 
 template <uint32_t WPS>
@@ -137,10 +144,11 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   // tile, at 33,792 B, cost a v_or per level: 8 of ~60 VALU per sample)
   // 8-B records (WPS 2) read a 16-B-stride copy of the first 16 entries: level k's byte
   // offset is then one shift-and-mask of the winners word (below)
-  __shared__ float lds_sum[4 * 16 + 3 * (kDeferUnit + 1) + kSumThreads * kSumSlot];
+  constexpr uint32_t kTable = 4u * 16u + 3u * (kDeferUnit + 1u);  // floats
+  __shared__ float lds_sum[kTable + kSumThreads * kSumSlot];
   float4* const att16 = reinterpret_cast<float4*>(lds_sum);
   float* const att_s = lds_sum + 4 * 16;  // KF_DEFER: attenuation rgb, entry kDeferUnit = 1
-  float* const tile = att_s + 3 * (kDeferUnit + 1);
+  float* const tile = lds_sum + kTable;
 #ifndef FR_SUM_PRIO
 #define FR_SUM_PRIO 0
 #endif
@@ -167,6 +175,13 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
   const bool mt = (kp.flags & FR_FLAG_MT_BANDS) != 0;
   const bool mt_zero = mt && !(kp.band_h && y / kp.band_h < 4u);  // rows render_mt never fills stay 0
   V3 sum = (first || !valid) ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
+#ifndef FR_SUM_WAITFIX
+#define FR_SUM_WAITFIX 1
+#endif
+  // The running sum's loads land here, before the first block's loads are issued. Left to
+  // the compiler, the wait for them sat on the first add of every block's sample loop,
+  // where (global loads complete in order) it also waited for the next block's prefetch.
+  if (FR_SUM_WAITFIX) asm volatile("" : "+v"(sum.x), "+v"(sum.y), "+v"(sum.z));
   const float fspp = static_cast<float>(kp.spp);
   const uint32_t per = WPS * kp.ks;  // floats per slot in the buffer
   // full 16-sample slots: block bl + 1's loads are issued before block bl is summed, so
@@ -181,7 +196,14 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
 #pragma unroll
     for (uint32_t k = 0; k < kV; ++k) {
       const uint32_t i = t + k * kSumThreads;
-      if (i < n4) v[k] = src4[i];
+      if (FR_SUM_WAITFIX) {
+        // every lane loads (past the last slot: the last float4 again), so the loads and
+        // the tile stores below are straight-line code: the wait before each store is for
+        // its own load, and no load waits for the one before it
+        v[k] = src4[min(i, n4 - 1u)];
+      } else if (i < n4) {
+        v[k] = src4[i];
+      }
     }
   };
   if (kp.ks == kBlockSamples && kp.nb) load_block(0);
@@ -192,7 +214,7 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
 #pragma unroll
       for (uint32_t k = 0; k < kV; ++k) {
         const uint32_t i = t + k * kSumThreads;
-        if (i < n4) {
+        if (FR_SUM_WAITFIX || i < n4) {  // (slots past nq are never read)
           const uint32_t slot = i / kV, w = (i - slot * kV) * 4u;
           float* d = tile + slot * kSumSlot + w;
           d[0] = v[k].x;
@@ -209,11 +231,20 @@ __global__ __launch_bounds__(kSumThreads) void sum_kernel(KParams kp, const floa
     if (valid && !mt_zero) {
       const uint32_t n = min(kBlockSamples, kp.spp - (kp.b0 + bl) * kBlockSamples);
       const float* c = tile + t * kSumSlot;
+      // FR_SUM_UNROLL (A/B): samples whose colour rebuilds interleave (the sums stay in order)
+#pragma unroll kSumUnroll
       for (uint32_t j = 0; j < n; ++j, c += WPS) {
         if (WPS == 2) {
           // 8-B record: terminal, then a_7 ... a_0 from 4-bit entries (kNibbleUnit: 1)
           const uint32_t tb = __float_as_uint(c[0]), w = __float_as_uint(c[1]);
+#if FR_SUM_SELECT
+          // the absorbed record's +0 by a select: no branch in the sample loop
+          const V3 sk = sky_from_t(c[0]);
+          const bool ab = tb == kDeferAbsorbed;
+          V3 col{ab ? 0.0f : sk.x, ab ? 0.0f : sk.y, ab ? 0.0f : sk.z};
+#else
           V3 col = tb == kDeferAbsorbed ? V3{0.0f, 0.0f, 0.0f} : sky_from_t(c[0]);
+#endif
           // level k's entry at byte 16 x nibble k: odd levels are the high nibble of byte
           // k / 2 of w, even levels the high nibble of byte k / 2 of w << 4
           const uint32_t w4 = w << 4;

@@ -10,8 +10,13 @@ status=0
 for spec in "$@"; do
   name="${spec%%|*}"; rest="${spec#*|}"; secs="${rest%%|*}"; cmd="${rest#*|}"
   echo "=== [$name] $(date +%T) limit ${secs}s: $cmd"
+  # a progress line a minute while the step runs (a long parity test prints nothing until
+  # it ends); the step's own time limit still bounds it
+  ( while sleep 60; do echo "... [$name] $(date +%T) running" >> gpurun_out/heartbeat.log; done ) &
+  hb=$!
   timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
   rc=$?
+  kill "$hb" 2>/dev/null; wait "$hb" 2>/dev/null
   echo "=== [$name] rc=$rc"
   tail -n 25 "gpurun_out/$name.log"
   if [ $rc -ge 124 ]; then
