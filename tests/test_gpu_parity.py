@@ -990,6 +990,30 @@ def test_absorbed_paths_skip_unwind_only_when_exact(gpu, colors):
     assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
 
 
+@pytest.mark.parametrize("n,bright,diffuse", [(14, False, False), (14, False, True), (6, False, True),
+                                              (15, False, False), (14, True, False)])
+def test_absorbed_paths_in_both_record_formats(gpu, n, bright, diffuse, monkeypatch):
+    """Absorbed paths (a depth cap of 3; metal rejections when not diffuse) in scenes of up
+    to 15 primitives, one with an attenuation above 1: the 8-B records (4-bit winners) and
+    the 12-B records (FR_DEFER=1) give the oracle's bits."""
+    w, h, spp, depth = 48, 32, 5, 3
+    prims = random_scene(40 + n, n)
+    if diffuse:
+        for q in prims:
+            if q["material"] in (S.METAL, S.DIELECTRIC):
+                q["material"] = S.LAMBERTIAN
+    if bright:
+        prims[0]["color"] = np.array([1.5, 0.5, 0.5], np.float32)
+    sc = gpu.Scene.from_prims(prims)
+    mean, u8, st = gpu.render(sc, gpu.camera_new(w, h), w, h, spp, depth, seed=9)
+    omean, ou8, ocnt, _ = O.render(prims, O.camera_new(w, h), w, h, spp, depth, seed=9, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
+    monkeypatch.setenv("FR_DEFER", "1")
+    m12, _, _ = gpu.render(sc, gpu.camera_new(w, h), w, h, spp, depth, seed=9)
+    assert np.array_equal(mean.view(np.uint32), m12.view(np.uint32))
+
+
 @pytest.mark.parametrize("pipe,buf_gb,jit", [("1", None, False), ("2", None, False), ("3", None, False),
                                             ("5", None, False), ("2", "0.0002", False), ("3", None, "wait"),
                                             ("2", "0.0002", "wait")])

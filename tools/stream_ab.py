@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--shards", type=int, default=1)
     ap.add_argument("--shard", type=int, default=0)
+    ap.add_argument("--allow-diff", action="append", default=[],
+                    help="variant whose frame may differ (a measurement-only build)")
     a = ap.parse_args()
     specs = []
     for v in a.variants:
@@ -78,8 +80,9 @@ def main():
                 print(json.dumps({"variant": name, "error": out.stderr[-600:]}), flush=True)
                 sys.exit(1)
             r = json.loads(out.stdout.strip().splitlines()[-1])
-            ref = ref or r["sha"]
-            if r["sha"] != ref:
+            if name not in a.allow_diff:
+                ref = ref or r["sha"]
+            if r["sha"] != ref and name not in a.allow_diff:
                 print(json.dumps({"variant": name, "error": f"frame hash {r['sha']} != {ref}"}), flush=True)
                 sys.exit(1)
             res[name].append(r)
