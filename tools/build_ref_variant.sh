@@ -21,7 +21,13 @@ mkdir -p "$root/fo-rma_amd/build/ab"
 FP="-ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP -fno-slp-vectorize $defs \
   -c "$tmp/fo-rma_amd/csrc/render.hip" -o "$tmp/render.o"
+objs="$tmp/render.o"
+if [ -f "$tmp/fo-rma_amd/csrc/sum.hip" ]; then  # sum_kernel's own unit (round 4 on)
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP -fno-slp-vectorize $defs \
+    -c "$tmp/fo-rma_amd/csrc/sum.hip" -o "$tmp/sum.o"
+  objs="$objs $tmp/sum.o"
+fi
 b="$root/fo-rma_amd/build"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$b/ab/libforma_rt_$name.so" "$tmp/render.o" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$b/ab/libforma_rt_$name.so" $objs \
   "$b/scene.o" "$b/json_min.o" "$b/bvh.o" "$b/post.o" "$b/jit.o" -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 echo "$b/ab/libforma_rt_$name.so"
