@@ -407,12 +407,12 @@ struct fr_ctx {
   // frame slots (sample buffer half, counter set), so frame k+1's trace starts when frame k's
   // trace ends while frame k's sum runs beside it; ev_fslot[s] = the end of the last sum
   // that used slot s, which the next frame on that slot waits for.
-  static constexpr int kFrameSlots = 3;
+  static constexpr int kFrameSlots = 4;  // at most (FR_FRAME_SLOTS, default 2)
   int frame_slot = 0, frame_parity = 0;
-  int fs_n = 0;            // slots in the current layout (2 or 3; 0: not pipelined)
+  int fs_n = 0;            // slots in the current layout (2 to 4; 0: not pipelined)
   size_t fs_bytes = 0;     // sample-buffer bytes per slot in that layout
-  hipEvent_t ev_fslot[kFrameSlots] = {nullptr, nullptr, nullptr};
-  bool fslot_used[kFrameSlots] = {false, false, false};
+  hipEvent_t ev_fslot[kFrameSlots] = {};
+  bool fslot_used[kFrameSlots] = {};
   unsigned long long* d_wcnt = nullptr;  // per-wave partial counters (KWork::wave_counters)
   uint32_t wcnt_waves = 0;               // their capacity in waves
   float* d_samples = nullptr;
@@ -716,6 +716,7 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
       hipEventCreateWithFlags(&c->ev_fslot[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fslot[1], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fslot[2], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fslot[3], hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&c->d_cnt, fr_ctx::kFrameSlots * 32 * sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&c->d_wcnt, fr_ctx::kFrameSlots * 3 * sizeof(unsigned long long) * kMaxWgPerCu * (kBlock / 64u) *
                                 c->num_cus) !=
@@ -903,13 +904,18 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   // one's drain leaves idle: shard 0/8 2.47 -> 2.29 ms per frame, 0/4 4.27-4.46 -> 4.28
   // (steadier), the same at N = 1 and 2, where serial traces keep each launch's own event
   // time. FR_FRAME_PIPE=1 / 2 forces serial / overlapping traces.
-  // Three slots when the budget holds them (a sum beside a trace runs about as long as the
-  // trace, so frame k + 2 would otherwise wait for frame k's sum), else two.
+  // Two slots (FR_FRAME_SLOTS=3 or 4 asks for more when the budget holds them). With round
+  // 3's sum, which ran longer than the trace beside it, three slots let frame k + 2's trace
+  // start before frame k's sum ended; since round 4's sum keeps pace, two are faster (C3
+  // streamed 16.27 -> 16.17 ms per frame, N = 2 shards -0.3 %, N = 4 and 8 the same).
   const char* fp_env = getenv("FR_FRAME_PIPE");
-  const int nfs = passes != 1 || (fp_env && strcmp(fp_env, "0") == 0) ? 0
-                  : cap_blocks >= 3u * nblocks                        ? 3
-                  : cap_blocks >= 2u * nblocks                        ? 2
-                                                                      : 0;
+  int want_fs = 2;
+  if (const char* e = getenv("FR_FRAME_SLOTS"))
+    want_fs = std::max(2, std::min(fr_ctx::kFrameSlots, atoi(e)));
+  int nfs = 0;
+  if (passes == 1 && !(fp_env && strcmp(fp_env, "0") == 0))
+    for (int k = want_fs; k >= 2 && !nfs; --k)
+      if (cap_blocks >= static_cast<uint64_t>(k) * nblocks) nfs = k;
   const bool fpipe = nfs > 0;
   const uint64_t grid_lanes = static_cast<uint64_t>(c->num_cus) * (kMaxWgPerCu - 1u) * kBlock;
   const bool fpipe_overlap =

@@ -552,16 +552,20 @@ def test_streamed_frames_match_the_oracle(gpu, shard, pipe, monkeypatch):
     ctx.close()
 
 
-@pytest.mark.parametrize("jit,pipe", [(False, "1"), ("wait", "1"), (False, "2"), ("wait", "2")])
-def test_pipelined_frames_of_different_seeds(gpu, jit, pipe, monkeypatch):
+@pytest.mark.parametrize("jit,pipe,slots", [(False, "1", None), ("wait", "1", None), (False, "2", None),
+                                           ("wait", "2", None), (False, "1", "3"), ("wait", "2", "4")])
+def test_pipelined_frames_of_different_seeds(gpu, jit, pipe, slots, monkeypatch):
     """Five frames of different seeds enqueued back to back with the frame pipeline, each
-    gathered into its own pinned frame: every gather holds its own frame (the two frame
-    slots are reused every other frame), equal to the frame rendered alone."""
+    gathered into its own pinned frame: every gather holds its own frame (the frame slots,
+    two by default, FR_FRAME_SLOTS 3 or 4, are reused in turn), equal to the frame rendered
+    alone."""
     w, h, spp, depth = 64, 40, 33, 8
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
     seeds = [3, 4, 5, 6, 7]
     refs = [gpu.render(sc, sc.camera, w, h, spp, depth, seed=sd) for sd in seeds]
     monkeypatch.setenv("FR_FRAME_PIPE", pipe)
+    if slots:
+        monkeypatch.setenv("FR_FRAME_SLOTS", slots)
     ctx = gpu.RenderContext(0)
     frames = [gpu.PinnedFrame(w, h) for _ in seeds]
     for sd, fr_ in zip(seeds, frames):
