@@ -1076,7 +1076,12 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       }
       unsigned long long* wcnt = c->d_wcnt + static_cast<size_t>(slot) * 3 * kMaxWgPerCu * (kBlock / 64u) * c->num_cus;
       kw.wave_counters = wcnt;
-      HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), ts));
+#ifndef FR_QUEUE_MEMSET
+#define FR_QUEUE_MEMSET 0
+#endif
+      // a pipelined frame's queue head is cnt[31], cleared with its counters above (before
+      // ev_start, which stream2 waits for); passes of a multi-pass frame reuse two heads
+      if (!fpipe || FR_QUEUE_MEMSET) HIPCHK(hipMemsetAsync(kw.queue, 0, sizeof(uint32_t), ts));
       HIPCHK(hipEventRecord(c->ev_trace[2 * traced], ts));
       if (c->log_on) HIPCHK(log_start(c, 0, ts));
       rc = launch_trace(dc->kinds, dc->has_plane, use_bvh, small_depth, grid, lds, ts, KArgs{ks, kc, kp, kw}, &jr);
