@@ -1021,25 +1021,33 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   c->t0 = std::chrono::steady_clock::now();
   // the last frame that used this slot's counters and samples (or, after a layout change,
   // every earlier frame) has been summed
+#ifndef FR_SETUP_ON_TRACE_STREAM
+#define FR_SETUP_ON_TRACE_STREAM 1
+#endif
+  // The frame's setup (slot wait, counter clear, start events) goes on the stream its trace
+  // runs on: with overlapping traces (stream2 every other frame) a setup on c->stream would
+  // wait behind the previous frame's whole trace there, and so would this frame's trace.
+  hipStream_t setup = c->stream;
+  if (FR_SETUP_ON_TRACE_STREAM && fpipe && fpipe_overlap && c->frame_parity) setup = c->stream2;
   for (int k = 0; k < fr_ctx::kFrameSlots; ++k)
-    if (c->fslot_used[k] && (k == fs || relayout)) HIPCHK(hipStreamWaitEvent(c->stream, c->ev_fslot[k], 0));
+    if (c->fslot_used[k] && (k == fs || relayout)) HIPCHK(hipStreamWaitEvent(setup, c->ev_fslot[k], 0));
   c->fs_n = nfs;
   c->fs_bytes = slot_bytes;
-  HIPCHK(hipMemsetAsync(cnt, 0, 32 * sizeof(unsigned long long), c->stream));
+  HIPCHK(hipMemsetAsync(cnt, 0, 32 * sizeof(unsigned long long), setup));
 #ifdef FR_DIAG
   {
     const unsigned long long z[2] = {0, 0};
-    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fr_diag_lens), z, sizeof(z), 0, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fr_diag_rus), z, sizeof(z), 0, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fr_diag_lens), z, sizeof(z), 0, hipMemcpyHostToDevice, setup));
+    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fr_diag_rus), z, sizeof(z), 0, hipMemcpyHostToDevice, setup));
     void* tc = nullptr;
     HIPCHK(hipGetSymbolAddress(&tc, HIP_SYMBOL(g_fr_tb_cost)));
-    HIPCHK(hipMemsetAsync(tc, 0, (1u << 20) * sizeof(unsigned int), c->stream));
+    HIPCHK(hipMemsetAsync(tc, 0, (1u << 20) * sizeof(unsigned int), setup));
   }
 #endif
-  HIPCHK(hipEventRecord(c->ev0, c->stream));
-  if (c->log_on) HIPCHK(log_start(c, 1, c->stream));
-  HIPCHK(hipEventRecord(c->ev_start, c->stream));
-  HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
+  HIPCHK(hipEventRecord(c->ev0, setup));
+  if (c->log_on) HIPCHK(log_start(c, 1, setup));
+  HIPCHK(hipEventRecord(c->ev_start, setup));
+  if (setup != c->stream2) HIPCHK(hipStreamWaitEvent(c->stream2, c->ev_start, 0));
   HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_start, 0));
   const uint32_t sum_blocks = (kp.P + kSumThreads - 1u) / kSumThreads;
   int traced = 0;  // trace launches whose events were recorded
