@@ -42,8 +42,8 @@ __global__ __launch_bounds__(kSumThreads) FR_SUM_VGPR_CAP void sum_kernel(KParam
                                                           float* __restrict__ running, float* __restrict__ out_mean,
                                                           uint8_t* __restrict__ out_u8, int first, int last,
                                                           const float4* __restrict__ att, uint32_t n_prims) {
-  constexpr uint32_t kSumSlot = WPS * kBlockSamples + 1;
-  constexpr int kUnroll = KIND == 1 ? kSumUnrollSkyd : kSumUnroll;  // floats per slot in LDS (odd stride)
+  constexpr uint32_t kSumSlot = WPS * kBlockSamples + 1;  // floats per slot in LDS (odd stride)
+  constexpr int kUnroll = KIND == 1 ? kSumUnrollSkyd : kSumUnroll;
   // one LDS block, the attenuation table first: its entries then sit at LDS byte offset
   // 12 x index, and the per-level reads need no base-address add (the table behind the
   // tile, at 33,792 B, cost a v_or per level: 8 of ~60 VALU per sample)
@@ -59,8 +59,8 @@ __global__ __launch_bounds__(kSumThreads) FR_SUM_VGPR_CAP void sum_kernel(KParam
 #endif
   // Pipelined frames run this kernel on the CU slot the next frame's
   // trace leaves free, where it takes about as long as the trace. A raised wave priority
-  // (FR_SUM_PRIO=3) made it keep pace but slowed the trace by 4 % (C3 streamed 16.65 ->
-  // 17.07 ms per frame): not used.
+  // slowed the trace by more than it sped the sum (FR_SUM_PRIO=3: C3 streamed 16.65 ->
+  // 17.07 ms per frame in round 3; 1: 16.26 -> 16.73 in round 4): not used.
   if (FR_SUM_PRIO) __builtin_amdgcn_s_setprio(FR_SUM_PRIO);
 #ifdef FR_SUM_STUB
   return;  // measurement-only builds (tools/stream_ab.py --allow-diff): the frame without its sum
