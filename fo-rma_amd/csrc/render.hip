@@ -1077,10 +1077,13 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       uint32_t blocks = 0;
       Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy, &blocks,
                 use_bvh && stage_n > 1 && !FR_BVH_RSTAGE ? kBlock * stage_n * 3 * sizeof(float) : 0u};
-      // pipelined frames leave room on every CU for the previous frame's sum workgroups
+      // pipelined frames leave room on every CU for the previous frame's sum workgroups:
+      // one slot, or two for shards whose traces overlap (N >= 4: each frame's sum is then
+      // short enough that the trace does better with it out of its way; shard 1/8 2.23 ->
+      // 2.18 ms per frame, 1/4 4.25 -> 4.19; at N = 1 two cost 6 %)
       if (fpipe) {
         const char* r = getenv("FR_FRAME_PIPE_RESERVE");
-        grid.reserve = r ? static_cast<uint32_t>(atoi(r)) : 1u;
+        grid.reserve = r ? static_cast<uint32_t>(atoi(r)) : fpipe_overlap ? 2u : 1u;
       }
       unsigned long long* wcnt = c->d_wcnt + static_cast<size_t>(slot) * 3 * kMaxWgPerCu * (kBlock / 64u) * c->num_cus;
       kw.wave_counters = wcnt;
