@@ -148,7 +148,8 @@ __global__ void ops_kernel(int op, const float* a, const float* b, uint32_t n, f
     case 9: r = div_rn(x, y, 1.0f / y); break;  // the kernel's jitter division
     case 10: r = recip_nr_ok(x) ? recip_nr(x) : 1.0f / x; break;
     case 11: r = fmax3_num(x, y, b[(i + 1) % n]); break;  // vs fmaxf(fmaxf(x, y), z)
-    case 12: r = fmin_num(fmin_num(x, y), b[(i + 1) % n]); break;
+    case 12: r = fmin3_num(x, y, b[(i + 1) % n]); break;  // vs fminf(fminf(x, y), z)
+    case 17: r = fmin_num(fmin_num(x, y), b[(i + 1) % n]); break;  // chained v_min_f32
     case 13: r = fmax_num(fmax_num(x, y), b[(i + 1) % n]); break;  // chained v_max_f32
     case 14: {  // sky_t_fast against sky_t on the direction (x, y, z = b[i + 1]): 0 when equal bits
       const V3 dv{x, y, b[(i + 1) % n]};
@@ -534,6 +535,9 @@ static std::string jit_defines() {
 #endif
 #ifdef FR_PROF
   d += "#define FR_PROF\n";  // section clocks go to the launch's counters, not device globals
+#endif
+#ifdef FR_SECCNT
+  d += "#define FR_SECCNT\n";  // region entry counts go to the launch's counters (tools/isa_sections.py)
 #endif
   return d;
 }
@@ -1160,6 +1164,11 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
       fprintf(stderr, "FR_PROF {\"claim\": %.4f, \"reject\": %.4f, \"hit\": %.4f, \"shade\": %.4f, \"end\": %.4f, "
               "\"wave_cycles\": %.4e}\n", cnt[20] / tot, cnt[21] / tot, cnt[22] / tot, cnt[23] / tot, cnt[24] / tot, tot);
     }
+#endif
+#ifdef FR_SECCNT
+    fprintf(stderr, "FR_SECCNT [");
+    for (int k = 0; k < SC_N; ++k) fprintf(stderr, k ? ", %llu" : "%llu", cnt[20 + k]);
+    fprintf(stderr, "]\n");
 #endif
 #ifdef FR_DIAG
     unsigned long long dl[2], dr[2];

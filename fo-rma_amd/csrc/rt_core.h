@@ -220,15 +220,36 @@ FR_HD int plane_test(V3 pos, V3 orient, V3 size, V3 o, V3 d, float t_min, float 
 // whose near (far) value equals tn (tf): -sign(d_k) on entry, +sign(d_k) on exit,
 // with sign(0) counted negative. Zero signs never matter (t is only compared, never 0
 // when accepted), so the hardware min/max agree with the host's fminf/fmaxf.
-FR_HD float fmin_num(float a, float b) { return fminf(a, b); }
+// v_min_f32 / v_max_f32 / v_min3_f32 directly: the generic lowering of fminf/fmaxf
+// re-canonicalises operands it cannot prove canonical (every result of an asm statement),
+// one v_max_f32 x, x, x per shared slab value in the scene kernel's list walk
+FR_HD float fmin_num(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return fminf(a, b);
+#endif
+}
 FR_HD float fmax_num(float a, float b) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  // v_max_f32 directly: the generic lowering re-canonicalises both operands first
   float r;
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 #else
   return fmaxf(a, b);
+#endif
+}
+// minNum(minNum(a, b), c) in one v_min3_f32 (device-checked against the chained v_min_f32
+// and the host's fminf chain: test_device_max3_and_min3_match_fmaxf_fminf)
+FR_HD float fmin3_num(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return fminf(fminf(a, b), c);
 #endif
 }
 
@@ -356,7 +377,7 @@ FR_HD Slab slab3(V3 lo, V3 hi, V3 o, V3 inv) {
   s.t0 = V3{(lo.x - o.x) * inv.x, (lo.y - o.y) * inv.y, (lo.z - o.z) * inv.z};
   s.t1 = V3{(hi.x - o.x) * inv.x, (hi.y - o.y) * inv.y, (hi.z - o.z) * inv.z};
   s.tn = fmax3_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y), fmin_num(s.t0.z, s.t1.z));
-  s.tf = fmin_num(fmin_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y)), fmax_num(s.t0.z, s.t1.z));
+  s.tf = fmin3_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y), fmax_num(s.t0.z, s.t1.z));
   return s;
 }
 
@@ -367,7 +388,7 @@ FR_HD Slab slab3_fused(V3 lo, V3 hi, V3 oinv, V3 inv) {
   s.t0 = V3{fmaf(lo.x, inv.x, -oinv.x), fmaf(lo.y, inv.y, -oinv.y), fmaf(lo.z, inv.z, -oinv.z)};
   s.t1 = V3{fmaf(hi.x, inv.x, -oinv.x), fmaf(hi.y, inv.y, -oinv.y), fmaf(hi.z, inv.z, -oinv.z)};
   s.tn = fmax3_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y), fmin_num(s.t0.z, s.t1.z));
-  s.tf = fmin_num(fmin_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y)), fmax_num(s.t0.z, s.t1.z));
+  s.tf = fmin3_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y), fmax_num(s.t0.z, s.t1.z));
   return s;
 }
 
@@ -395,9 +416,12 @@ FR_HD V3 slab_normal(const Slab& s, float t, V3 dd) {
   // the first axis whose near (entry) or far (exit) distance equals t; the sign is
   // -sign(d_k) on entry and +sign(d_k) on exit, sign(0) counted negative. Selects on lane
   // masks instead of a divergent branch in which both cases ran for a mixed wave.
+  // (both per-axis extremes formed up front: a conditional asm min/max became a branch)
   const bool entry = t == s.tn;
-  const bool kx = entry ? fmin_num(s.t0.x, s.t1.x) == t : fmax_num(s.t0.x, s.t1.x) == t;
-  const bool ky = !kx && (entry ? fmin_num(s.t0.y, s.t1.y) == t : fmax_num(s.t0.y, s.t1.y) == t);
+  const float mnx = fmin_num(s.t0.x, s.t1.x), mxx = fmax_num(s.t0.x, s.t1.x);
+  const float mny = fmin_num(s.t0.y, s.t1.y), mxy = fmax_num(s.t0.y, s.t1.y);
+  const bool kx = (entry ? mnx : mxx) == t;
+  const bool ky = !kx && (entry ? mny : mxy) == t;
   const bool kz = !kx && !ky;
   const float dk = kx ? dd.x : (ky ? dd.y : dd.z);
   const float sg = ((dk > 0.0f) != entry) ? 1.0f : -1.0f;

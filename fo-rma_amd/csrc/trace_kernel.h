@@ -297,12 +297,37 @@ enum { PF_CLAIM, PF_REJ, PF_HIT, PF_SHADE, PF_END, PF_N };
 #define PROF_MARK(k) do {} while (0)
 #endif
 
+// Per-phase instruction accounting (tools/isa_sections.py; never in the product). The lane
+// loop is cut into regions at SEC(k):
+//   FR_SEC_MARKS: SEC(k) is an assembler comment, so the ISA listing (hipcc -S) can be split
+//                 into regions and each region's VALU instructions counted (static);
+//   FR_SECCNT:    SEC(k) counts the wave-level entries of region k (first active lane, an LDS
+//                 add; per launch into counters[20 + k]) (dynamic).
+// Static VALU per region x wave entries per region = the launch's VALU instructions by phase.
+// The first SC_N regions are counted; the others only mark a boundary in the listing, and
+// their entries follow from a counted one (SETUP ~ CLAIM, ACC = NEED, POSTHIT = HIT,
+// POSTSHADE = LATCH = ITER; GRAB = the batches the queue hands out).
+enum { SC_ITER, SC_CLAIM, SC_JIT, SC_NEED, SC_REJ, SC_CAM, SC_SCAT, SC_HIT, SC_SKY, SC_SHADE, SC_END, SC_N,
+       SC_GRAB = SC_N, SC_SETUP, SC_ACC, SC_POSTHIT, SC_POSTSHADE, SC_LATCH };
+#if defined(FR_SEC_MARKS) && defined(__HIP_DEVICE_COMPILE__)
+#define SEC(k) asm volatile(";FRSEC " #k)
+#elif defined(FR_SECCNT)
+#define SEC(k)                                                                       \
+  do {                                                                               \
+    const unsigned long long m_ = __ballot(1);                                       \
+    if ((k) < SC_N && lane == static_cast<uint32_t>(__ffsll(m_) - 1))              \
+      atomicAdd(&sec_cnt[(k) < SC_N ? (k) : 0], 1u);                               \
+  } while (0)
+#else
+#define SEC(k) do {} while (0)
+#endif
+
 // HAS_PLANE: planes may leave the shared record's t/p stale (plane.rs:27-29), so
 // the last written t is tracked separately from the winner's.
 // (two 32-bit popcounts: a 64-bit one leaves a 64-bit count whose compare the SALU
 // cannot do, and the compiler moved it to the VALU)
 __device__ __forceinline__ uint32_t lanes_set(bool b) {
-  const unsigned long long m = __ballot(b);
+  const unsigned long long m = __builtin_amdgcn_ballot_w64(b);
   return static_cast<uint32_t>(__builtin_popcount(static_cast<uint32_t>(m)) +
                                __builtin_popcount(static_cast<uint32_t>(m >> 32)));
 }
@@ -496,6 +521,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     g_fr_wave_drain[gw] = ~0ull;
   }
 #endif
+#ifdef FR_SECCNT
+  __shared__ uint32_t sec_cnt[SC_N];
+  if (tid < SC_N) sec_cnt[tid] = 0;
+#endif
   __syncthreads();
 
 
@@ -570,6 +599,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     held_b = bb;
   }
   while (active) {
+    SEC(SC_ITER);
     DIAG_WAVE(DG_ITER);
 #ifdef FR_DIAG
     if (lane == 0 && (gw & 63u) == 0 && (gw >> 6) < 1024u && diag_iter < 1024u)
@@ -583,6 +613,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     // Only when work starts changes, never what a sample computes (results bit-identical).
     constexpr uint32_t CLAIM_MIN = NIB ? FR_CLAIM_MIN_NIB : FR_CLAIM_MIN;
     if (m && (CLAIM_MIN <= 1 || lanes_set(need_item) >= CLAIM_MIN || m == __ballot(1))) {
+      SEC(SC_CLAIM);
       // 0. claim work items: the free lanes take consecutive items of the wave's batch;
       // when it runs out, the first free lane reserves the next batch of kBatch = 64
       // items (one tile of one sample block) globally. n <= 64, so one batch suffices.
@@ -608,6 +639,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       uint32_t xy = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_xy)));
       uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_b)));
       if (grab) {
+        SEC(SC_GRAB);
         if (static_cast<int>(lane) == first) base = atomicAdd(kw.queue, kBatch);
         base = __builtin_amdgcn_readlane(base, first);
         // A slot past the image or the queue gets a stream that is never used.
@@ -658,6 +690,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         continue;
       }
       if (need_item) {
+        SEC(SC_SETUP);
         const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
         bool ok = xy != 0xFFFFFFFFu;
         uint32_t yrow = kp.H - y;  // tracer.rs:171-172: v = ((H - y) + r) / H
@@ -691,6 +724,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       }
     }
     if (need_jit) {
+      SEC(SC_JIT);
       // a sample starts: jitter (tracer.rs:171-172), then its lens sample in step 1. One
       // place for the first sample of a block and the next sample of the same block, so
       // the wave runs it once per iteration
@@ -708,11 +742,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     uint32_t tsky = kDeferAbsorbed;  // DEFER: the terminal as sky parameter bits (SKYD: dot(d, d))
     float sky_dy = 0.0f;             // SKYD: the escaping ray's d.y
     if (need != NEED_NONE) {
+      SEC(SC_NEED);
       // 1. merged rejection loop
       float px = 0.0f, py = 0.0f, pz = 0.0f;
       bool acc = false;
       const bool sph = need == NEED_SPHERE;
       do {
+        SEC(SC_REJ);
         DIAG_WAVE(DG_LENS_W);
         DIAG_LANE(DG_LENS_L);
         if (!acc) {
@@ -723,11 +759,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           acc = !(px * px + py * py + pz * pz >= kUnitBallScaled);
         }
       } while (lanes_set(!acc) > static_cast<uint32_t>(KREJ));
+      SEC(SC_ACC);
       if (acc) {
         px *= kSignedUnitScale;  // the accepted point, 2r - 1 per coordinate (exact)
         py *= kSignedUnitScale;
         pz *= kSignedUnitScale;
         if (!sph) {
+          SEC(SC_CAM);
           // Camera::get_ray (camera.rs:62-72)
 #if !defined(FR_CAM_RESIDENT) && defined(__HIP_DEVICE_COMPILE__)
           // scalar loads of the camera from the kernarg segment, here, rather than 19
@@ -750,6 +788,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           depth = 0;
           have_ray = true;
         } else {
+          SEC(SC_SCAT);
           const V3 r{px, py, pz};
           bool ok = true;
           V3 dir;
@@ -774,6 +813,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     }
     PROF_MARK(PF_REJ);
     if (have_ray) {
+      SEC(SC_HIT);
       // 2. closest hit over the list in order (tracer.rs:190-200): only the accepted t
       // of each test is needed here; the record is formed for the winner below.
       ++nseg;
@@ -1042,7 +1082,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         }
       }
       PROF_MARK(PF_HIT);
+      SEC(SC_POSTHIT);
       if (best < 0) {
+        SEC(SC_SKY);
         if (SKYD) {
           sky_dy = d.y;
           tsky = __float_as_uint(d.x * d.x + d.y * d.y + d.z * d.z);  // length()'s sum, in its order
@@ -1062,6 +1104,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         ended = true;  // unless a scatter continues the path
         have_ray = false;
         if (depth < kp.max_depth) {
+          SEC(SC_SHADE);
           // the shared HitRecord: normal of the winner at its own t; p = point_at(last t written)
           const V3 pw = add(o, scl(closest, d));
           // the winner's record and class: LDS when staged (n_rec / n_att are uniform;
@@ -1129,7 +1172,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       }
     }
     PROF_MARK(PF_SHADE);
+    SEC(SC_POSTSHADE);
     if (ended) {
+      SEC(SC_END);
       // 3. attenuation * get_color(...) (tracer.rs:206-207), innermost first
       DIAG_WAVE(DG_END_W);
       DIAG_LANE(DG_END_L);
@@ -1248,6 +1293,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         need_jit = true;  // next sample of the block, same stream
     }
     PROF_MARK(PF_END);
+    SEC(SC_LATCH);
   }
 
   // Per-wave counter reduction into the wave's own slot (plain stores): the waves leave
@@ -1265,6 +1311,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     wc[1] = b;
     wc[2] = sct;
   }
+#ifdef FR_SECCNT
+  __syncthreads();
+  if (tid < SC_N) atomicAdd(&kw.counters[20 + tid], static_cast<unsigned long long>(sec_cnt[tid]));
+#endif
 #ifdef FR_PROF
   if (lane == 0)
     for (int k = 0; k < PF_N; ++k) atomicAdd(&kw.counters[20 + k], static_cast<unsigned long long>(pf_acc[k]));

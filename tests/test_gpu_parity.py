@@ -81,11 +81,11 @@ def test_recip_nr_exhaustive(gpu):
 
 
 def test_device_max3_and_min3_match_fmaxf_fminf(gpu):
-    """The slab test's v_max3_f32 (tn) and the compiler's v_min3_f32 (tf) against the
-    host's fmaxf/fminf chains, bit for bit, on edge values (NaN, +-0, +-inf, denormals).
-    Slab distances come from arithmetic, which only makes quiet NaNs; signalling NaNs
-    (which IEEE-mode v_max quiets and propagates one step) are quieted for the host
-    comparison, and v_max3 must equal the chained v_max_f32 on them as on everything."""
+    """The slab test's v_max3_f32 (tn) and v_min3_f32 (tf) against the host's fmaxf/fminf
+    chains, bit for bit, on edge values (NaN, +-0, +-inf, denormals). Slab distances come
+    from arithmetic, which only makes quiet NaNs; signalling NaNs (which IEEE-mode v_max /
+    v_min quiet and propagate one step) are quieted for the host comparison, and v_max3 /
+    v_min3 must equal the chained v_max_f32 / v_min_f32 on them as on everything."""
     import ctypes as C
     rng = np.random.default_rng(12)
     fp = C.POINTER(C.c_float)
@@ -105,6 +105,7 @@ def test_device_max3_and_min3_match_fmaxf_fminf(gpu):
     x_raw = _edge_floats(rng, 50000)
     y_raw = np.roll(_edge_floats(rng, 50000), 3)[: x_raw.size]
     assert _same_bits(run(11, x_raw, y_raw), run(13, x_raw, y_raw))  # max3 == chained v_max, sNaN included
+    assert _same_bits(run(12, x_raw, y_raw), run(17, x_raw, y_raw))  # min3 == chained v_min, sNaN included
     x, y = quiet(x_raw), quiet(y_raw)
     z = np.roll(y, -1)
     for op, f in ((11, np.fmax), (12, np.fmin)):

@@ -16,8 +16,16 @@ if [ "$rev" = "." ]; then
 else
   git -C "$root" archive "$rev" fo-rma_amd/csrc include | tar -x -C "$tmp"
 fi
-make -C "$root/fo-rma_amd" -s build/scene.o build/json_min.o build/bvh.o build/post.o build/jit.o
+make -C "$root/fo-rma_amd" -s build/scene.o build/json_min.o build/bvh.o build/post.o
 mkdir -p "$root/fo-rma_amd/build/ab"
+# the scene-specialised kernel is compiled at run time from the sources embedded in jit.o:
+# embed REV's trace_kernel.h (and what it includes), so the A/B covers the hiprtc kernel too
+c="$tmp/fo-rma_amd/csrc"
+mkdir -p "$tmp/fo-rma_amd/build"
+python3 "$c/embed_sources.py" "$tmp/fo-rma_amd/build/jit_sources.inc" trace_kernel.h="$c/trace_kernel.h" \
+  rt_core.h="$c/rt_core.h" bvh.h="$c/bvh.h" forma_rt.h="$tmp/include/forma_rt.h"
+g++ -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function $defs -D__HIP_PLATFORM_AMD__ \
+  -I/opt/rocm/include -c "$c/jit.cpp" -o "$tmp/jit.o"
 FP="-ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $FP -fno-slp-vectorize $defs \
   -c "$tmp/fo-rma_amd/csrc/render.hip" -o "$tmp/render.o"
@@ -29,5 +37,5 @@ if [ -f "$tmp/fo-rma_amd/csrc/sum.hip" ]; then  # sum_kernel's own unit (round 4
 fi
 b="$root/fo-rma_amd/build"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$b/ab/libforma_rt_$name.so" $objs \
-  "$b/scene.o" "$b/json_min.o" "$b/bvh.o" "$b/post.o" "$b/jit.o" -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
+  "$b/scene.o" "$b/json_min.o" "$b/bvh.o" "$b/post.o" "$tmp/jit.o" -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 echo "$b/ab/libforma_rt_$name.so"
