@@ -108,7 +108,7 @@ def shard_rows(height, shard, shards, strip=8):
 
 
 def gather_frame(mean_rgb, rank, world, height, strip=8):
-    """Stitch every rank's strips into rank 0's image (--verify only, after timing).
+    """Stitch every rank's strips into rank 0's image (after timing).
     `mean_rgb` is this rank's full-size [H, W, 3] buffer with only its own strips valid.
     Returns the stitched frame on rank 0, None elsewhere."""
     import numpy as np
@@ -500,6 +500,27 @@ def frame_hash(mean):
     return hashlib.sha256(mean.tobytes()).hexdigest()[:16]
 
 
+def compare_with_n1(stitched, n1):
+    """The N > 1 line's self-check: the frame stitched from the N shards against the same
+    frame rendered whole on one device (the RNG is keyed by global pixel, so the strips of
+    tracer.rs:83-134's row tiling must give the N = 1 image bit for bit)."""
+    a, b = frame_hash(stitched), frame_hash(n1)
+    return {"frame_sha256_16": a, "n1_frame_sha256_16": b, "frame_matches_n1": a == b}
+
+
+def render_n1_frame(fr, device, scene, cam, no_scene_jit):
+    """The whole frame on one context of `device` (after the timed region): the N = 1
+    reference for compare_with_n1."""
+    ctx = fr.RenderContext(device)
+    try:
+        ctx.render(scene, cam, fr.make_params(WIDTH, HEIGHT, SPP, DEPTH, SEED, scene_jit=not no_scene_jit))
+        ctx.sync()
+        mean, _ = ctx.download(WIDTH, HEIGHT)
+    finally:
+        ctx.close()
+    return mean
+
+
 def run_mctx(a, plan, torch, fr):
     """N > 1 in one process: fr_mctx over plan["devices"], shard i of N on entry i, every
     frame's strips gathered asynchronously into the context's page-locked host frame.
@@ -563,7 +584,9 @@ def run_mctx(a, plan, torch, fr):
         frames_ms = c.trace_log_read(frames=True)
         c.trace_log(False)
         shards.append({"shard": i, "device": devices[i], "samples": st["samples"], "segments": st["segments"],
-                       "hits": st["hits"], "scatters": st["scatters"], "trace_launches": st["trace_launches"],
+                       "hits": st["hits"], "scatters": st["scatters"],
+                       "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
+                       "trace_launches": st["trace_launches"],
                        "occupancy": st["occupancy"],
                        "trace_ms_per_launch": round(sum(launches_ms) / max(1, len(launches_ms)), 4),
                        "trace_ms_min_max": [round(min(launches_ms), 4), round(max(launches_ms), 4)]
@@ -580,7 +603,8 @@ def run_mctx(a, plan, torch, fr):
     roof, hbm = rooflines({k: slow[k] for k in ("segments", "hits", "scatters", "samples")}, kinds, pixels,
                           len(scene), launches, launch_ms)
     roof["shard"] = slow["shard"]
-    out = base_line(a, n, value, elapsed, f"row-strips x{n}, one process, fr_mctx over devices {devices}")
+    out = base_line(a, n, value, elapsed, f"row-strips x{n}, one process, fr_mctx over devices {devices}"
+                    + (" (REHEARSAL: devices repeat)" if rehearsal else ""))
     out.update({
         "launch": "one process (fr_mctx), no launcher" + (" — REHEARSAL: devices repeat, timing is not an "
                                                            "N-GPU measurement" if rehearsal else ""),
@@ -601,9 +625,9 @@ def run_mctx(a, plan, torch, fr):
                          "get_ms": [round(j["ms"], 1) for j in jits], "prepare_ms": round(prepare_ms, 1)},
         "roofline": roof,
         "hbm_roofline": hbm,
-        "frame_sha256_16": frame_hash(mean),
     })
     mc.close()
+    out.update(compare_with_n1(mean, render_n1_frame(fr, devices[0], scene, cam, a.no_scene_jit)))
     return out
 
 
@@ -661,11 +685,13 @@ def run_rank(a, plan, torch, fr):
     total_segs = barrier.sum(counts["segments"] * n)
     pixels = len(shard_rows(HEIGHT, rank, world)) * WIDTH
 
-    checksum = None
-    if a.verify or world == 1:
-        frame_img = gather_frame(frame.mean, rank, world, HEIGHT)
-        if rank == 0:
-            checksum = frame_hash(frame_img)
+    # every run reports its frame's hash; N > 1 stitches the shards on rank 0 (after the timed
+    # region) and checks them against the whole frame rendered on rank 0's device
+    frame_img = gather_frame(frame.mean, rank, world, HEIGHT)
+    check = None
+    if rank == 0:
+        check = ({"frame_sha256_16": frame_hash(frame_img)} if world == 1 else
+                 compare_with_n1(frame_img, render_n1_frame(fr, local, scene, cam, a.no_scene_jit)))
     if rank != 0:
         return None
     pmc = pmc_in_run(scene_jit=jit["used"]) if (world == 1 and not a.no_pmc) else {}
@@ -701,8 +727,7 @@ def run_rank(a, plan, torch, fr):
     })
     if pmc:
         out["pmc"] = pmc
-    if checksum:
-        out["frame_sha256_16"] = checksum
+    out.update(check)
     if world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.cpu_budget)
         out["speedup_vs_cpu_baseline"] = round(value / out["cpu_baseline"]["value"], 1)
@@ -726,7 +751,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--verify", action="store_true", help="stitch the frame on rank 0 and report a checksum")
+    ap.add_argument("--verify", action="store_true",
+                    help="(kept for old command lines: every run now reports its frame hash, and N > 1 checks it "
+                         "against the N = 1 frame)")
     ap.add_argument("--sync-each", action="store_true", help="wait for each frame's stats before the next")
     ap.add_argument("--no-scene-jit", action="store_true",
                     help="run the compiled-in trace kernel instead of the scene-specialised one (same image)")

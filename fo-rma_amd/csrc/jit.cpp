@@ -44,6 +44,7 @@
 
 #include "internal.h"
 #include "jit.h"
+#include "jit_cache.h"
 #include "../build/jit_sources.inc"
 
 namespace fr {
@@ -63,15 +64,6 @@ const char* const kOpts[] = {"-O3",
                              "-fno-gpu-flush-denormals-to-zero",
                              "-fno-slp-vectorize"};
 
-uint64_t fnv1a(const void* p, size_t n, uint64_t h) {
-  const unsigned char* b = static_cast<const unsigned char*>(p);
-  for (size_t i = 0; i < n; ++i) {
-    h ^= b[i];
-    h *= 0x100000001b3ull;
-  }
-  return h;
-}
-
 std::string hex_key(const std::string& text) {
   // two independent 64-bit FNV-1a lanes: a 128-bit key
   const uint64_t a = fnv1a(text.data(), text.size(), 0xcbf29ce484222325ull);
@@ -81,8 +73,10 @@ std::string hex_key(const std::string& text) {
   return buf;
 }
 
-// FR_JIT_OPTS: extra compiler options, space-separated (A/B experiments only)
-std::vector<std::string> extra_opts() {
+// FR_JIT_OPTS: extra compiler options, space-separated (A/B experiments only). Read once:
+// the cache key (toolchain_tag) and every compile use this one snapshot, so a process that
+// changes the variable later cannot store code built with other options under the key.
+std::vector<std::string> parse_extra_opts() {
   std::vector<std::string> extra;
   if (const char* e = getenv("FR_JIT_OPTS")) {
     std::string cur;
@@ -97,6 +91,11 @@ std::vector<std::string> extra_opts() {
     }
   }
   return extra;
+}
+
+const std::vector<std::string>& extra_opts() {
+  static const std::vector<std::string> v = parse_extra_opts();
+  return v;
 }
 
 // What else decides the code object besides the sources and the records: the option list,
@@ -132,86 +131,6 @@ std::string cache_dir() {
   return d;
 }
 
-bool read_file(const std::string& path, std::vector<char>& out) {
-  FILE* f = fopen(path.c_str(), "rb");
-  if (!f) return false;
-  fseek(f, 0, SEEK_END);
-  const long n = ftell(f);
-  fseek(f, 0, SEEK_SET);
-  out.resize(n > 0 ? static_cast<size_t>(n) : 0u);
-  const bool ok = n > 0 && fread(out.data(), 1, out.size(), f) == out.size();
-  fclose(f);
-  return ok;
-}
-
-// A disk-cache file is a 32-B header — magic, format version, code size, a 128-bit hash of
-// the code — then the code object. The HIP loader does not reject a damaged code object: it
-// aborts the process (a truncated file did, on the GPU box). So nothing read from disk
-// reaches hipModuleLoadData unless its size and hash check out.
-constexpr char kCacheMagic[4] = {'F', 'R', 'J', 'C'};
-constexpr uint32_t kCacheFormat = 1;
-constexpr size_t kCacheHeader = 32;
-
-void code_hash(const char* p, size_t n, uint64_t h[2]) {
-  h[0] = fnv1a(p, n, 0xcbf29ce484222325ull);
-  h[1] = fnv1a(p, n, 0x84222325cbf29ce4ull ^ n);
-}
-
-std::vector<char> wrap_code(const std::vector<char>& code) {
-  std::vector<char> out(kCacheHeader + code.size());
-  const uint64_t size = code.size();
-  uint64_t h[2];
-  code_hash(code.data(), code.size(), h);
-  memcpy(out.data(), kCacheMagic, 4);
-  memcpy(out.data() + 4, &kCacheFormat, 4);
-  memcpy(out.data() + 8, &size, 8);
-  memcpy(out.data() + 16, h, 16);
-  if (!code.empty()) memcpy(out.data() + kCacheHeader, code.data(), code.size());
-  return out;
-}
-
-// The code object of a cache file, or false (a damaged or foreign file: removed).
-bool read_cached_code(const std::string& path, std::vector<char>& code) {
-  std::vector<char> raw;
-  if (!read_file(path, raw)) return false;
-  uint32_t fmt = 0;
-  uint64_t size = 0, h[2] = {0, 0}, want[2];
-  bool ok = raw.size() > kCacheHeader && memcmp(raw.data(), kCacheMagic, 4) == 0;
-  if (ok) {
-    memcpy(&fmt, raw.data() + 4, 4);
-    memcpy(&size, raw.data() + 8, 8);
-    memcpy(want, raw.data() + 16, 16);
-    ok = fmt == kCacheFormat && size == raw.size() - kCacheHeader;
-  }
-  if (ok) {
-    code_hash(raw.data() + kCacheHeader, static_cast<size_t>(size), h);
-    ok = h[0] == want[0] && h[1] == want[1];
-  }
-  if (!ok) {
-    unlink(path.c_str());
-    return false;
-  }
-  code.assign(raw.begin() + kCacheHeader, raw.end());
-  return true;
-}
-
-// The file appears under `path` only when every byte reached the disk: a failed write,
-// flush or close (a full disk) leaves no truncated code object behind.
-bool write_file_atomic(const std::string& path, const std::vector<char>& data) {
-  const std::string tmp = path + ".tmp." + std::to_string(getpid());
-  FILE* f = fopen(tmp.c_str(), "wb");
-  if (!f) return false;  // an unwritable cache only costs the next process a compile
-  bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
-  ok = fflush(f) == 0 && ok;
-  ok = fsync(fileno(f)) == 0 && ok;
-  ok = fclose(f) == 0 && ok;
-  if (!ok || rename(tmp.c_str(), path.c_str()) != 0) {
-    unlink(tmp.c_str());
-    return false;
-  }
-  return true;
-}
-
 // Keep at most kMaxDiskFiles code objects in the cache directory: the oldest go first.
 void prune_disk(const std::string& dir) {
   DIR* d = opendir(dir.c_str());
@@ -245,8 +164,7 @@ int compile(const std::string& arch, const std::string& prelude, const char* nam
   const std::string arch_opt = "--offload-arch=" + arch;
   std::vector<const char*> all{arch_opt.c_str()};
   for (const char* o : kOpts) all.push_back(o);
-  const std::vector<std::string> extra = extra_opts();
-  for (const std::string& x : extra) all.push_back(x.c_str());
+  for (const std::string& x : extra_opts()) all.push_back(x.c_str());
   const hiprtcResult r = hiprtcCompileProgram(prog, static_cast<int>(all.size()), all.data());
   if (r != HIPRTC_SUCCESS) {
     size_t n = 0;
@@ -321,12 +239,20 @@ struct CodeEntry {
   uint64_t used = 0;
 };
 
+// A module's last launch: jit_note_launch records it (an event on the launch's stream); an
+// evicted module is unloaded after that event, not after a drain of the whole device.
+// (The event is destroyed when its module is unloaded, never at process exit: the runtime
+// may be gone by then.)
+struct ModuleUse {
+  hipEvent_t last = nullptr;
+};
+
 struct Module {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr;
   int device = 0;
   uint64_t used = 0;
-  std::shared_ptr<void> pin = std::make_shared<char>(0);  // copies held by callers (JitStats::pin)
+  std::shared_ptr<ModuleUse> pin = std::make_shared<ModuleUse>();  // copies held by callers (JitStats::pin)
 };
 
 struct Job {  // a background compile: everything copied, nothing borrowed from the caller
@@ -438,14 +364,19 @@ const std::string& toolchain() {
   return t;
 }
 
-// Unload a module evicted from the table once its device has drained: a launch of it may
-// still be queued on a stream. No caller holds it (unpinned): a render that looked it up
-// holds its pin from the lookup through the launch.
+// Unload a module evicted from the table once its last launch has finished: a launch of it
+// may still be queued on a stream (its event, jit_note_launch). No caller holds it
+// (unpinned): a render that looked it up holds its pin from the lookup through the launch
+// and the event record, so no launch of it can follow.
 void unload_evicted(const Module& m) {
   int cur = -1;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(m.device);
-  (void)hipDeviceSynchronize();
+  if (m.pin->last) {
+    (void)hipEventSynchronize(m.pin->last);
+    (void)hipEventDestroy(m.pin->last);
+    m.pin->last = nullptr;
+  }
   (void)hipModuleUnload(m.mod);
   if (cur >= 0) (void)hipSetDevice(cur);
 }
@@ -470,7 +401,18 @@ int jit_wait_all() {
   return FR_OK;
 }
 
-int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* out, JitStats* stats) {
+void jit_note_launch(const std::shared_ptr<void>& pin, hipStream_t stream) {
+  ModuleUse* u = static_cast<ModuleUse*>(pin.get());
+  if (!u) return;
+  if (!u->last && hipEventCreateWithFlags(&u->last, hipEventDisableTiming) != hipSuccess) {
+    u->last = nullptr;
+    return;
+  }
+  (void)hipEventRecord(u->last, stream);
+}
+
+int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* out, JitStats* stats,
+                     bool cached_only) {
   const auto t0 = std::chrono::steady_clock::now();
   JitStats st;
   auto done = [&](int state) {
@@ -511,6 +453,15 @@ int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* 
       if (attempt == 0 && !path.empty() && read_cached_code(path, bytes)) {
         lk.lock();
         R.finish(key, FR_OK, std::move(bytes), "", true);
+      } else if (cached_only && !wait) {
+        lk.lock();
+        auto e = R.code.find(key);
+        if (e != R.code.end() && e->second.state == CodeEntry::kCompiling) {
+          R.code.erase(e);  // nothing was started for it
+          --R.compiling;
+          R.cv.notify_all();
+        }
+        return done(FR_JIT_MISS);
       } else if (wait) {
         const int rc = compile_checked(arch, prelude, spec.name_expr, mname, bytes);
         const std::string err = rc ? fr_last_error() : "";
@@ -528,7 +479,7 @@ int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* 
       if (it == R.code.end()) return set_error(FR_EHIP, "scene kernel code object evicted while loading");
     }
     if (it->second.state == CodeEntry::kCompiling) {
-      if (!wait) return done(FR_JIT_PENDING);
+      if (!wait) return done(cached_only ? FR_JIT_MISS : FR_JIT_PENDING);
       R.cv.wait(lk, [&] {
         auto e = R.code.find(key);
         return e == R.code.end() || e->second.state != CodeEntry::kCompiling;

@@ -43,7 +43,15 @@ struct JitStats {
 // background worker and FR_OK returns with *out = nullptr and stats->state PENDING (or
 // FAILED after a failed compile): the caller runs the compiled-in kernel, whose image is
 // the same bits.
-int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* out, JitStats* stats);
+// cached_only (wait = false): a code object in this process or on disk is used, as above;
+// otherwise nothing is compiled or queued: *out = nullptr, stats->state FR_JIT_MISS (a
+// one-shot caller then neither waits for hiprtc nor leaves a compile for process exit).
+int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* out, JitStats* stats,
+                     bool cached_only = false);
+
+// After a launch of a module's kernel on `stream`: the module is unloaded (LRU eviction)
+// only after this launch has finished (an event on the stream, not a device drain).
+void jit_note_launch(const std::shared_ptr<void>& pin, hipStream_t stream);
 
 // Block until the background worker has no compile queued or running.
 int jit_wait_all();

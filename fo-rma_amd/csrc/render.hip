@@ -197,9 +197,12 @@ __global__ void recip_check_kernel(uint64_t base, uint64_t count, unsigned long 
   }
 }
 
-__global__ void rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
+// the trace kernel's seeding (rng_seed2): the scatter stream, or with camera the camera stream
+__global__ void rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out, int camera) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  Rng r = rng_seed(seed, pixel, sample);
+  Rng sr, cr;
+  rng_seed2(seed, pixel, sample, sr, cr);
+  Rng r = camera ? cr : sr;
   for (uint32_t i = 0; i < n; ++i) out[i] = rng_next(r);
 }
 
@@ -485,6 +488,8 @@ struct Grid {
 struct JitReq {
   bool on = false;
   bool wait = false;  // compile on this thread if needed (fr_ctx_prepare, FR_FLAG_SCENE_JIT_WAIT)
+  bool cached_only = false;  // FR_FLAG_SCENE_JIT_CACHED: never compile or queue (one-shot callers)
+  std::shared_ptr<void> pin;  // the scene kernel's module: its launches are noted (jit_note_launch)
   int device = 0;
   const DeviceCopy* dc = nullptr;
   bool dry = false;   // fr_ctx_prepare: get the kernel, launch nothing
@@ -508,6 +513,9 @@ static std::string jit_defines() {
   def("FR_BLOCK_SAMPLES", FR_BLOCK_SAMPLES);
   def("FR_FINE_SAMPLES", FR_FINE_SAMPLES);
   def("FR_STAGE", FR_STAGE);
+  def("FR_CAMB", FR_CAMB);
+  def("FR_CAM_MIN", FR_CAM_MIN);
+  def("FR_KLENS", FR_KLENS);
   def("FR_BVH_STAGE", FR_BVH_STAGE);
 #ifdef FR_TRACE_PRIO
   def("FR_TRACE_PRIO", FR_TRACE_PRIO);
@@ -554,7 +562,7 @@ static int launch_persistent(const Grid& g, size_t lds, hipStream_t st, KArgs a,
       const int targs[8] = {KS, HP, KREJ, MAXD, BV, MT, DEFER, MAT};
       const bool tbool[8] = {false, true, false, false, true, true, false, false};
       const JitSpec spec{name, targs, tbool, 8, jit_defines(), jr->dc->rec_words.data(), jr->dc->n};
-      const int rc = jit_trace_kernel(jr->device, spec, jr->wait, &jr->fn, &jr->stats);
+      const int rc = jit_trace_kernel(jr->device, spec, jr->wait, &jr->fn, &jr->stats, jr->cached_only);
       if (rc) return rc;
       jr->resolved = true;
     }
@@ -599,6 +607,7 @@ static int launch_persistent(const Grid& g, size_t lds, hipStream_t st, KArgs a,
     size_t bytes = sizeof(KArgs);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
     HIPCHK(hipModuleLaunchKernel(jfn, blocks, 1, 1, kBlock, 1, 1, static_cast<uint32_t>(lds), st, nullptr, cfg));
+    jit_note_launch(jr->pin, st);  // an LRU eviction of the module waits for this launch only
   } else {
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, st, a);
   }
@@ -965,8 +974,11 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
                                                sizeof(uint32_t);
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
   const size_t stage_n = stage_samples(use_bvh);
-  const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * wps * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
-                     n_rec * 64 + stack_bytes + (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
+  // the kernel's camera-batching slots (trace_kernel.h camb_kernel): 24 B per lane
+  const bool camb = camb_kernel(nibble ? 2 : defer ? 1 : 0, use_bvh);
+  const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * wps * sizeof(float) : 0u) +
+                     (camb ? kBlock * kCamSlotFloats * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 + n_rec * 64 +
+                     stack_bytes + (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
   // the scene-specialised kernel (jit.h): list-loop scenes of <= kJitMaxPrims primitives,
   // when the caller asks (FR_FLAG_SCENE_JIT; FR_SCENE_JIT=1 / 0 forces it on / off)
   JitReq jr;
@@ -984,6 +996,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     // prepare, FR_FLAG_SCENE_JIT_WAIT and the environment's FR_SCENE_JIT=1 wait for the
     // compile; plain FR_FLAG_SCENE_JIT renders run the compiled-in kernel until it is done
     jr.wait = dry || (p->flags & FR_FLAG_SCENE_JIT_WAIT) != 0 || (je && *je && strcmp(je, "0") != 0);
+    jr.cached_only = !jr.wait && (p->flags & FR_FLAG_SCENE_JIT_CACHED) != 0;
   }
   KWork kw;
   kw.counters = cnt;
@@ -994,6 +1007,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   if (jr.on && kp.P && c->jc_fn && c->jc_uid == dc->uid && c->jc_flags == jc_flags && c->jc_small == small_depth) {
     jr.resolved = true;
     jr.fn = c->jc_fn;
+    jr.pin = c->jc_pin;
     jit_got.reused = 1;
     jit_got.state = FR_JIT_USED;
   } else if (jr.on && kp.P) {
@@ -1008,6 +1022,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     jit_got = pre.stats;
     jr.resolved = pre.resolved;
     jr.fn = pre.fn;
+    jr.pin = pre.stats.pin;
     c->jc_fn = pre.fn;  // null (pending or failed): looked up again next render
     c->jc_pin = pre.stats.pin;
     c->jit_stats.pin.reset();
@@ -1167,7 +1182,7 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
 #endif
 #ifdef FR_SECCNT
     fprintf(stderr, "FR_SECCNT [");
-    for (int k = 0; k < SC_N; ++k) fprintf(stderr, k ? ", %llu" : "%llu", cnt[20 + k]);
+    for (int k = 0; k < SC_N; ++k) fprintf(stderr, k ? ", %llu" : "%llu", cnt[4 + k]);
     fprintf(stderr, "]\n");
 #endif
 #ifdef FR_DIAG
@@ -1218,10 +1233,13 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
     HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     const fr_params& p = c->last;
     const uint32_t strips = (p.height + kStripRows - 1) / kStripRows;
-    uint64_t rows = 0;
+    uint64_t rows = 0, traced_rows = 0;
+    // render_mt never traces the rows past 4 * (H / 4) (tracer.rs:87)
+    const uint32_t mt_end = (p.flags & FR_FLAG_MT_BANDS) ? (p.height / 4u) * 4u : p.height;
     for (uint32_t k = p.shard_index; k < strips; k += p.shard_count) {
       const uint32_t r0 = k * kStripRows, r1 = r0 + kStripRows < p.height ? r0 + kStripRows : p.height;
       rows += r1 - r0;
+      traced_rows += r1 <= mt_end ? r1 - r0 : r0 < mt_end ? mt_end - r0 : 0u;
     }
     st->segments = cnt[0];
     st->hits = cnt[1];
@@ -1237,7 +1255,9 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
     st->trace_ms = tms;
     st->trace_launches = static_cast<uint32_t>(c->passes);
     st->occupancy = static_cast<uint32_t>(c->occupancy);
-    st->scatters = cnt[2];
+    // every path traces one segment more than it scatters (tracer.rs:189-210: each scatter
+    // is followed by one more get_color), so the kernel counts segments and hits only
+    st->scatters = cnt[0] - traced_rows * p.width * static_cast<uint64_t>(p.spp);
     st->total_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t0).count();
   }
@@ -1590,16 +1610,25 @@ int fr_selftest_ops(int device, int op, const float* a, const float* b, uint32_t
   return FR_OK;
 }
 
-int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
+static int selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out,
+                        int camera) {
   if (!out) return set_error(FR_EARG, "fr_selftest_rng: null buffer");
   SET_DEVICE(device);
   uint32_t* d = nullptr;
   HIPCHK(hipMalloc(&d, (n ? n : 1) * sizeof(uint32_t)));
-  hipLaunchKernelGGL(rng_kernel, dim3(1), dim3(64), 0, 0, seed, pixel, sample, n, d);
+  hipLaunchKernelGGL(rng_kernel, dim3(1), dim3(64), 0, 0, seed, pixel, sample, n, d, camera);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(out, d, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIPCHK(hipFree(d));
   return FR_OK;
+}
+
+int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
+  return selftest_rng(device, seed, pixel, sample, n, out, 0);
+}
+
+int fr_selftest_rng_camera(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
+  return selftest_rng(device, seed, pixel, sample, n, out, 1);
 }
 
 /* Diagnostic: exhaustive recip_nr check over [base, base + count) bit patterns;

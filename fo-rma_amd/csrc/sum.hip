@@ -105,15 +105,16 @@ __global__ __launch_bounds__(kSumThreads) FR_SUM_VGPR_CAP void sum_kernel(KParam
     // 192-B (128-B) slots: 16-B aligned
     const float4* src4 = reinterpret_cast<const float4*>(samples + WPS * (static_cast<size_t>(bl * kp.P + q0) * kp.ks));
     if (FR_SUM_BUFLOAD) {
-      // buffer loads: one 32-bit lane offset for all kV loads (the block's offsets in the
-      // scalar operand) instead of a 64-bit address per load; the descriptor's range
-      // (the workgroup's n4 float4) returns 0 past the last slot
+      // buffer loads: a 32-bit lane offset per load instead of a 64-bit address; the
+      // descriptor's range (the workgroup's n4 float4) returns 0 past the last slot. The
+      // whole offset is in the lane operand: the raw-buffer range check covers the lane
+      // offset, and the scalar offset may be outside it on this family
       const __amdgpu_buffer_rsrc_t r =
           __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(src4), 0, static_cast<int>(n4 * 16u), 0x00020000);
       typedef float v4f __attribute__((ext_vector_type(4)));
 #pragma unroll
       for (uint32_t k = 0; k < kV; ++k) {
-        const v4f x = __builtin_amdgcn_raw_buffer_load_b128(r, t * 16u, k * kSumThreads * 16u, 0);
+        const v4f x = __builtin_amdgcn_raw_buffer_load_b128(r, t * 16u + k * kSumThreads * 16u, 0, 0);
         v[k] = make_float4(x.x, x.y, x.z, x.w);
       }
       return;

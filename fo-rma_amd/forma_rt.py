@@ -35,7 +35,8 @@ FR_FLAG_WRITE_U8 = 1
 FR_FLAG_MT_BANDS = 2  # save_image_mt semantics (forma_rt.h)
 FR_FLAG_SCENE_JIT = 4  # scene-specialised trace kernel (hiprtc, cached; same image bits)
 FR_FLAG_SCENE_JIT_WAIT = 8  # ... compiled on the render's thread when missing (else in the background)
-FR_JIT_OFF, FR_JIT_USED, FR_JIT_PENDING, FR_JIT_FAILED = 0, 1, 2, 3  # fr_ctx_jit_state
+FR_FLAG_SCENE_JIT_CACHED = 16  # ... only when already built or on disk; never compiled (one-shot callers)
+FR_JIT_OFF, FR_JIT_USED, FR_JIT_PENDING, FR_JIT_FAILED, FR_JIT_MISS = 0, 1, 2, 3, 4  # fr_ctx_jit_state
 MAX_DEPTH = 50  # tracer.rs:10
 DEFAULT_SEED = 0x5EED
 
@@ -88,7 +89,7 @@ EXPORTS = (
     "fr_ctx_wait", "fr_ctx_device_buffers", "fr_host_alloc", "fr_host_free", "fr_ctx_trace_log",
     "fr_ctx_trace_log_read", "fr_mctx_create", "fr_mctx_free", "fr_mctx_count", "fr_mctx_ctx", "fr_mctx_render",
     "fr_mctx_sync", "fr_mctx_frame", "fr_mctx_download",
-    "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_recip",
+    "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_rng_camera", "fr_selftest_recip",
     "fr_post_process", "fr_post_process_device", "fr_rgb_to_rgba_device", "fr_ctx_jit_info", "fr_selftest_jit",
     "fr_ctx_prepare", "fr_ctx_jit_state", "fr_jit_wait",
 )
@@ -167,6 +168,7 @@ def lib():
     L.fr_render_hip_multi.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
     L.fr_selftest_ops.argtypes = [C.c_int, C.c_int, f3, f3, C.c_uint32, f3]
     L.fr_selftest_rng.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+    L.fr_selftest_rng_camera.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
     if hasattr(L, "fr_post_process"):  # absent from A/B builds of older sources
         L.fr_post_process.argtypes = [C.c_int, P(C.c_int), C.c_uint32, C.c_float, C.c_uint32, C.c_uint32,
                                       P(C.c_uint8), P(C.c_uint8)]
@@ -404,12 +406,14 @@ def scene_path(name):
 def make_params(width, height, spp, max_depth=MAX_DEPTH, seed=DEFAULT_SEED, shard_index=0, shard_count=1,
                 write_u8=True, mt_bands=False, scene_jit=False):
     """scene_jit: False, True (the scene kernel once it is compiled; until then renders run
-    the compiled-in kernel, same bits) or "wait" (compile on the render's thread if needed)."""
+    the compiled-in kernel, same bits), "wait" (compile on the render's thread if needed) or
+    "cached" (the scene kernel only if already built or on disk; never a compile)."""
     p = FrParams()
     p.width, p.height, p.spp, p.max_depth, p.seed = width, height, spp, max_depth, seed
     p.strip_rows, p.shard_index, p.shard_count = 8, shard_index, shard_count
     p.flags = ((FR_FLAG_WRITE_U8 if write_u8 else 0) | (FR_FLAG_MT_BANDS if mt_bands else 0) |
-               (FR_FLAG_SCENE_JIT if scene_jit else 0) | (FR_FLAG_SCENE_JIT_WAIT if scene_jit == "wait" else 0))
+               (FR_FLAG_SCENE_JIT if scene_jit else 0) | (FR_FLAG_SCENE_JIT_WAIT if scene_jit == "wait" else 0) |
+               (FR_FLAG_SCENE_JIT_CACHED if scene_jit == "cached" else 0))
     return p
 
 
@@ -758,7 +762,9 @@ def save_image_mt(model, sample, path="out/basic_mt.png", max_depth=MAX_DEPTH):
     scene, scenes::get_simple_scene, with the model's camera), each pass gamma-corrected
     to u8, the u8 frames averaged and truncated, PNG."""
     simple = Scene.builtin(0, model.width, model.height)
-    acc, u8, stats = model.render(simple, sample, max_depth, model.seed, mt_bands=True, scene_jit=True)
+    # a one-shot call: the scene kernel if it is cached, never a compile (which a process that
+    # exits after this call would wait for at exit)
+    acc, u8, stats = model.render(simple, sample, max_depth, model.seed, mt_bands=True, scene_jit="cached")
     write_png(path, u8)
     return acc, u8, stats
 
@@ -766,6 +772,6 @@ def save_image_mt(model, sample, path="out/basic_mt.png", max_depth=MAX_DEPTH):
 def save_image(model, sample, path="out/basic.png", max_depth=MAX_DEPTH):
     """tracer.rs:160-187: `sample` spp per pixel, gamma 2, u8, PNG. Like the reference it
     fails if the output directory is missing (tracer.rs:186 unwrap)."""
-    mean, u8, stats = model.render(model.scene, sample, max_depth, model.seed, scene_jit=True)
+    mean, u8, stats = model.render(model.scene, sample, max_depth, model.seed, scene_jit="cached")
     write_png(path, u8)
     return mean, u8, stats

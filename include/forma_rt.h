@@ -99,11 +99,17 @@ extern "C" {
    instead (FR_SCENE_JIT=0 turns it off for every render). */
 #define FR_FLAG_SCENE_JIT 4u
 #define FR_FLAG_SCENE_JIT_WAIT 8u /* with FR_FLAG_SCENE_JIT: compile on the render's thread if needed */
+/* with FR_FLAG_SCENE_JIT (not _WAIT): use the scene kernel only if its code object is in this
+   process or the disk cache; never compile or queue a compile (FR_JIT_MISS otherwise). For
+   one-shot callers: a queued background compile runs to its end when the process exits, so
+   a process that renders once and exits would otherwise wait for hiprtc at exit. */
+#define FR_FLAG_SCENE_JIT_CACHED 16u
 /* fr_ctx_jit_state: which trace kernel the last render (or fr_ctx_prepare) ran */
 #define FR_JIT_OFF 0     /* compiled-in kernel: not asked for, a BVH scene, or > 64 primitives */
 #define FR_JIT_USED 1    /* the scene-specialised kernel */
 #define FR_JIT_PENDING 2 /* asked for, compile still running: the compiled-in kernel ran */
 #define FR_JIT_FAILED 3  /* asked for, compile failed: the compiled-in kernel ran */
+#define FR_JIT_MISS 4    /* asked for cached only (FR_FLAG_SCENE_JIT_CACHED), none cached: compiled-in kernel */
 
 /*
  * One primitive, in the order it is tested (list order decides ties, tracer.rs:195-200).
@@ -307,7 +313,10 @@ int fr_rgb_to_rgba_device(void* stream, const uint8_t* d_rgb, uint8_t* d_rgba, s
 /* Run the device f32/RNG primitives on n inputs (op codes in DESIGN.md §7); used by the
    parity tests to show the GPU arithmetic is bit-identical to the host's. */
 int fr_selftest_ops(int device, int op, const float* a, const float* b, uint32_t n, float* out);
+/* The first n words of the scatter stream (fr_selftest_rng) and of the camera stream
+   (fr_selftest_rng_camera) of (seed, pixel, stream key = sample) as the kernel seeds them. */
 int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out);
+int fr_selftest_rng_camera(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out);
 /* Compare the device's fast reciprocal (rcp + one Newton step) with the correctly rounded
    1.0f / x for every f32 bit pattern in [base, base + count): mismatches per exponent
    field in bad[256], first mismatching pattern in first[256] (0xFFFFFFFF = none). */

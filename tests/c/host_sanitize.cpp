@@ -11,6 +11,11 @@
 //                                  (plain and forced) and a tiny oracle render of it
 //   host_sanitize spheres N        N spheres on a grid (fr_scene_create) through the BVH
 //                                  builder, plain and forced
+//   host_sanitize cache FILE...    each file through the scene kernel's disk-cache reader
+//                                  (fo-rma_amd/csrc/jit_cache.cpp read_cached_code, the
+//                                  guard in front of the HIP loader); a file that passes is
+//                                  re-wrapped and must equal itself byte for byte
+//   host_sanitize wrap N OUT       a valid cache file around N bytes of code
 // One JSON line per input on stdout.
 #include <stdint.h>
 #include <stdio.h>
@@ -23,6 +28,7 @@
 #include "../../include/forma_rt.h"
 #include "../../fo-rma_amd/csrc/bvh.h"
 #include "../../fo-rma_amd/csrc/internal.h"
+#include "../../fo-rma_amd/csrc/jit_cache.h"
 
 // A host-only build makes no device copies of a scene: fr_scene_free has none to release.
 namespace fr {
@@ -124,13 +130,33 @@ static int do_spheres(uint32_t n) {
   return rc == FR_OK ? 0 : 1;
 }
 
+static int do_cache(const char* path) {
+  std::vector<char> raw, code;
+  const bool had = fr::read_file(path, raw);
+  const bool ok = fr::read_cached_code(path, code);
+  bool same = false;
+  if (ok) same = fr::wrap_code(code) == raw;
+  printf("{\"file\": \"%s\", \"readable\": %d, \"ok\": %d, \"code_bytes\": %zu, \"rewrap_equal\": %d}\n", path,
+         had ? 1 : 0, ok ? 1 : 0, code.size(), same ? 1 : 0);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 3 && strcmp(argv[1], "cache") == 0) {
+    for (int i = 2; i < argc; ++i) do_cache(argv[i]);
+    return 0;
+  }
+  if (argc == 4 && strcmp(argv[1], "wrap") == 0) {
+    std::vector<char> code(static_cast<size_t>(atoi(argv[2])));
+    for (size_t i = 0; i < code.size(); ++i) code[i] = static_cast<char>(i * 131u + 7u);
+    return fr::write_file_atomic(argv[3], fr::wrap_code(code)) ? 0 : 1;
+  }
   if (argc >= 3 && strcmp(argv[1], "json") == 0) {
     for (int i = 2; i < argc; ++i)
       if (do_json(argv[i])) return 2;
     return 0;
   }
   if (argc == 3 && strcmp(argv[1], "spheres") == 0) return do_spheres(static_cast<uint32_t>(atoi(argv[2])));
-  fprintf(stderr, "usage: %s json FILE... | spheres N\n", argv[0]);
+  fprintf(stderr, "usage: %s json FILE... | spheres N | cache FILE... | wrap N OUT\n", argv[0]);
   return 2;
 }

@@ -55,3 +55,25 @@ def test_frame_hash_is_the_rehearsal_checksum():
     import numpy as np
     m = np.zeros((4, 5, 3), np.float32)
     assert bench.frame_hash(m) == bench.frame_hash(m.copy()) and len(bench.frame_hash(m)) == 16
+
+
+def test_n_gt_1_line_checks_its_stitched_frame_against_n1():
+    """The driver's SCALE lines (N = 2, 4, 8) check themselves: rank 0 stitches the shards'
+    strips (bench.gather_frame) and compares them with the frame rendered whole on its device
+    (bench.compare_with_n1): equal frames report frame_matches_n1 = true, and a frame whose
+    one shard differs in one ulp of one channel reports false."""
+    import numpy as np
+    rng = np.random.default_rng(3)
+    h, w, n = 40, 6, 4
+    whole = rng.random((h, w, 3), dtype=np.float32)
+    stitched = np.zeros_like(whole)
+    for k in range(n):  # each shard's rows (8-row strips, k mod n), as gather_frame places them
+        rows = bench.shard_rows(h, k, n)
+        stitched[rows] = whole[rows]
+    r = bench.compare_with_n1(stitched, whole)
+    assert r["frame_matches_n1"] and r["frame_sha256_16"] == r["n1_frame_sha256_16"]
+    bad = stitched.copy()
+    y = bench.shard_rows(h, 3, n)[2]
+    bad[y, 1, 2] = np.nextafter(bad[y, 1, 2], np.float32(2.0))
+    r = bench.compare_with_n1(bad, whole)
+    assert not r["frame_matches_n1"] and r["frame_sha256_16"] != r["n1_frame_sha256_16"]

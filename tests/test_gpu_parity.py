@@ -266,6 +266,8 @@ def test_device_rng_matches_oracle(gpu, seed, pixel, sample):
     out = (C.c_uint32 * 200)()
     gpu.check(gpu.lib().fr_selftest_rng(0, seed, pixel, sample, 200, out))
     assert list(out) == list(O.rng_stream(seed, pixel, sample, 200))
+    gpu.check(gpu.lib().fr_selftest_rng_camera(0, seed, pixel, sample, 200, out))
+    assert list(out) == list(O.rng_stream(seed, pixel, sample, 200, camera=True))
 
 
 # ---- images -----------------------------------------------------------------------
@@ -717,9 +719,11 @@ def test_c2_full_frame(gpu):
 def test_c4_full_frame_every_shard_through_mctx(gpu, monkeypatch):
     """C4 (scene_08 3840x2160, 1024 spp, 8 bounces, row-tiled across 8 devices) as the
     drop-in renders it: one fr_mctx over 8 contexts (here all on device 0), the scene kernel,
-    the whole 8.49 G-sample frame stitched in the page-locked host frame. Every shard is
-    checked: 4 full 3,840-px rows of each against the oracle (spread over the shard's
-    strips), and the stitched frame's counters equal the sum of the eight shard renders'."""
+    the whole 8.49 G-sample frame stitched in the page-locked host frame. Against the oracle:
+    4 full 3,840-px rows of every shard (spread over its strips), and every one of the 2,160
+    rows at every 8th pixel (1.06 G samples: each strip of each shard, so every shard's
+    claims, sub-blocks and tiles); the stitched frame's counters equal the sum of the eight
+    shard renders'."""
     monkeypatch.setenv("FR_SAMPLE_BUFFER_GB", "12")  # one pass per shard, no frame slots: 8 x 8.5 GB
     w, h, spp, depth, n = 3840, 2160, 1024, 8, 8
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
@@ -746,6 +750,12 @@ def test_c4_full_frame_every_shard_through_mctx(gpu, monkeypatch):
                                   progress=_progress("C4 all shards"))
     assert_parity(mean, u8, None, omean, ou8, None, rows=rows)
     assert np.array_equal(mean[rows].view(np.uint32), omean[rows].view(np.uint32))
+    # every row, every 8th column
+    cmean, cu8, ccnt = O.render_rows(prims, cam, w, h, spp, depth, range(h), threads=oracle_threads(), col_step=8,
+                                     chunk=240, progress=_progress("C4 every row, col_step 8"))
+    assert ccnt["samples"] == h * (w // 8) * spp
+    assert_parity(mean[:, ::8], u8[:, ::8], None, cmean[:, ::8], cu8[:, ::8], None)
+    assert np.array_equal(mean[:, ::8].view(np.uint32), cmean[:, ::8].view(np.uint32))
 
 
 # ---- BVH (scenes of >= 48 primitives, <= 32 planes) -------------
@@ -1067,7 +1077,10 @@ def test_c4_shards_on_row_subsets(gpu, shard, buf_gb, monkeypatch):
 def test_c5_generator_scene_on_full_rows(gpu):
     """C5 (10k spheres, 1920x1080, 512 spp, 8 bounces, BVH path) against the oracle's
     brute-force list loop on 64 full rows spread over the image (every 17th row from 0),
-    122,880 pixels, 62.9 M samples (about 200 s of oracle on the GPU box's 16 CPUs)."""
+    122,880 pixels, 62.9 M samples, and on every row at every 32nd pixel (64,800 pixels,
+    33.2 M samples), so every region of the image's traversals is compared (about 300 s
+    of oracle on the GPU box's 16 CPUs). The BVH's list-order ties and padded t_max
+    (tracer.rs:195-200) must give the list loop's winner everywhere."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("gen_scene", os.path.join(ROOT, "tools", "gen_scene.py"))
     gs = importlib.util.module_from_spec(spec)
@@ -1084,6 +1097,10 @@ def test_c5_generator_scene_on_full_rows(gpu):
                                   progress=_progress("C5"))
     assert_parity(mean, u8, st, omean, ou8, None, rows=rows)
     assert np.isfinite(mean).all()
+    cmean, cu8, _ = O.render_rows(prims, cam, w, h, spp, depth, range(h), threads=oracle_threads(), col_step=32,
+                                  chunk=36, progress=_progress("C5 every row, col_step 32"))
+    assert_parity(mean[:, ::32], u8[:, ::32], None, cmean[:, ::32], cu8[:, ::32], None)
+    assert np.array_equal(mean[:, ::32].view(np.uint32), cmean[:, ::32].view(np.uint32))
 
 
 @pytest.mark.parametrize("depth", [8, 12])

@@ -1,5 +1,6 @@
-"""Host sanitizer build: the product's JSON parser, scene builder and BVH
-builder (fo-rma_amd/csrc/json_min.cpp, scene.cpp, bvh.cpp) and the oracle (oracle/oracle.cpp)
+"""Host sanitizer build: the product's JSON parser, scene builder, BVH builder
+and scene-kernel cache reader (fo-rma_amd/csrc/json_min.cpp, scene.cpp, bvh.cpp,
+jit_cache.cpp) and the oracle (oracle/oracle.cpp)
 compiled with -fsanitize=address,undefined -fno-sanitize-recover=all into one CPU program
 (tests/c/host_sanitize.cpp), then driven over every bundled scene, the generator's 10k-sphere
 scene (BASELINE config C5), a malformed-JSON corpus and a 150k-sphere BVH build. Any
@@ -23,7 +24,7 @@ FR_OK, FR_EARG, FR_EPARSE = 0, -1, -2
 def exe(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("asan") / "host_sanitize")
     srcs = [os.path.join(ROOT, "tests", "c", "host_sanitize.cpp")] + [
-        os.path.join(ROOT, "fo-rma_amd", "csrc", f) for f in ("json_min.cpp", "scene.cpp", "bvh.cpp")] + [
+        os.path.join(ROOT, "fo-rma_amd", "csrc", f) for f in ("json_min.cpp", "scene.cpp", "bvh.cpp", "jit_cache.cpp")] + [
         os.path.join(ROOT, "oracle", "oracle.cpp")]
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
                     "-fno-omit-frame-pointer", "-ffp-contract=off", "-fno-fast-math", "-pthread",
@@ -121,3 +122,46 @@ def test_malformed_json_corpus_fails_cleanly(exe, tmp_path):
 def test_150k_sphere_bvh_build_clean(exe):
     (r,) = _run(exe, "spheres", "150000")
     assert r["rc"] == FR_OK and r["bvh"]["ok"] == 1 and r["bvh"]["order"] == 150000
+
+
+def test_cache_file_reader_rejects_damaged_files_cleanly(exe, tmp_path):
+    """The scene kernel's disk-cache reader (jit_cache.cpp read_cached_code): the HIP loader
+    aborts the process on a damaged code object, so nothing reaches it unless the 32-B
+    header's magic, format, size and hash check out. A valid file round-trips; truncations,
+    byte flips in header and body, a wrong size field (too small, too large, 2^63), a wrong
+    magic or format, garbage, an empty file, a header alone, a directory and a missing file
+    are refused without a sanitizer report, and a refused file is removed."""
+    import struct
+    good = tmp_path / "good.hsaco"
+    subprocess.run([exe, "wrap", "5000", str(good)], check=True, timeout=60)
+    raw = good.read_bytes()
+    assert len(raw) == 5032
+    bad = {
+        "empty": b"",
+        "header_only": raw[:32],
+        "garbage": bytes(random.Random(3).randrange(256) for _ in range(4000)),
+        "bad_magic": b"XRJC" + raw[4:],
+        "bad_format": raw[:4] + struct.pack("<I", 2) + raw[8:],
+        "size_small": raw[:8] + struct.pack("<Q", 4999) + raw[16:],
+        "size_large": raw[:8] + struct.pack("<Q", 5001) + raw[16:],
+        "size_huge": raw[:8] + struct.pack("<Q", 1 << 63) + raw[16:],
+        "hash_flip": raw[:20] + bytes([raw[20] ^ 1]) + raw[21:],
+        "body_flip": raw[:1000] + bytes([raw[1000] ^ 0x80]) + raw[1001:],
+        "extra_byte": raw + b"\0",
+    }
+    for k, cut in enumerate((1, 31, 33, 100, len(raw) // 2, len(raw) - 1)):
+        bad[f"trunc_{k}"] = raw[:cut]
+    paths = []
+    for name, data in bad.items():
+        p = tmp_path / f"{name}.hsaco"
+        p.write_bytes(data)
+        paths.append(str(p))
+    (tmp_path / "a_directory.hsaco").mkdir()
+    paths += [str(tmp_path / "a_directory.hsaco"), str(tmp_path / "missing.hsaco")]
+    res = _run(exe, "cache", str(good), *paths)
+    assert res[0]["ok"] == 1 and res[0]["code_bytes"] == 5000 and res[0]["rewrap_equal"] == 1
+    for r in res[1:]:
+        assert r["ok"] == 0, r
+    for name in bad:
+        assert not (tmp_path / f"{name}.hsaco").exists(), name  # refused files are removed
+    assert (tmp_path / "a_directory.hsaco").is_dir()  # (a directory is not a file to remove)

@@ -339,3 +339,46 @@ def test_one_shot_save_image_through_mctx_on_a_cold_cache(gpu, tmp_path):
     assert r["bit_identical"], r
     assert r["cold_states"] == [2, 2] and r["hot_states"] == [1, 1], r
     assert r["ratio"] <= 1.5, r
+
+
+_ONE_SHOT = r'''
+import json, os, sys, time
+sys.path.insert(0, os.path.join(sys.argv[1], "fo-rma_amd"))
+import forma_rt as fr
+t0 = time.perf_counter()
+m = fr.create_model(320, 180, fr.Scene.from_file(fr.scene_path("scene_08"), 320, 180))
+if sys.argv[2] == "warm":  # compile the kernel save_image will look up, on this thread
+    m.render(m.scene, 8, fr.MAX_DEPTH, m.seed, scene_jit="wait")
+mean, u8, st = fr.save_image(m, 8, path=os.path.join(sys.argv[3], "one_shot.png"))
+print(json.dumps({"state": m.ctx.jit_state(), "ms": (time.perf_counter() - t0) * 1e3,
+                  "sha": __import__("hashlib").sha256(mean.tobytes()).hexdigest()[:16]}))
+'''
+
+
+@pytest.mark.gpu
+def test_one_shot_save_image_never_queues_a_compile(gpu, tmp_path):
+    """save_image / save_image_mt are one-shot calls (the reference's only caller renders once,
+    frontend/macroquad.rs:60): with FR_FLAG_SCENE_JIT_CACHED they use the scene kernel only if
+    its code object is cached and otherwise compile nothing, so a process that renders once
+    and exits never waits for hiprtc at exit (a queued background compile runs to its end
+    there). Cold cache: FR_JIT_MISS, no file written, the compiled-in kernel's bits. Warm
+    cache (the same kernel compiled earlier in the process): FR_JIT_USED, the same bits."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cache = tmp_path / "cache"
+    cache.mkdir()
+    env = dict(os.environ, FR_JIT_CACHE=str(cache))
+    env.pop("FR_SCENE_JIT", None)
+    res = {}
+    for mode in ("cold", "warm"):
+        out = subprocess.run([sys.executable, "-c", _ONE_SHOT, root, mode, str(tmp_path)], env=env, capture_output=True,
+                             text=True, timeout=300)
+        assert out.returncode == 0, out.stderr[-2000:]
+        res[mode] = json.loads(out.stdout.strip().splitlines()[-1])
+        if mode == "cold":
+            assert res[mode]["state"] == gpu.FR_JIT_MISS, res
+            assert not list(cache.iterdir()), "a cold one-shot save_image queued a compile"
+    assert res["warm"]["state"] == gpu.FR_JIT_USED, res
+    assert res["cold"]["sha"] == res["warm"]["sha"], res

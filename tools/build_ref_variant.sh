@@ -16,7 +16,7 @@ if [ "$rev" = "." ]; then
 else
   git -C "$root" archive "$rev" fo-rma_amd/csrc include | tar -x -C "$tmp"
 fi
-make -C "$root/fo-rma_amd" -s build/scene.o build/json_min.o build/bvh.o build/post.o
+make -C "$root/fo-rma_amd" -s build/scene.o build/json_min.o build/bvh.o build/post.o build/jit_cache.o
 mkdir -p "$root/fo-rma_amd/build/ab"
 # the scene-specialised kernel is compiled at run time from the sources embedded in jit.o:
 # embed REV's trace_kernel.h (and what it includes), so the A/B covers the hiprtc kernel too
@@ -37,5 +37,5 @@ if [ -f "$tmp/fo-rma_amd/csrc/sum.hip" ]; then  # sum_kernel's own unit (round 4
 fi
 b="$root/fo-rma_amd/build"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$b/ab/libforma_rt_$name.so" $objs \
-  "$b/scene.o" "$b/json_min.o" "$b/bvh.o" "$b/post.o" "$tmp/jit.o" -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
+  "$b/scene.o" "$b/json_min.o" "$b/bvh.o" "$b/post.o" "$b/jit_cache.o" "$tmp/jit.o" -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 echo "$b/ab/libforma_rt_$name.so"

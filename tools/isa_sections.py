@@ -24,14 +24,14 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "fo-rma_amd", "csrc")
 # counted regions, in trace_kernel.h's SC_* order
-REGIONS = ["SC_ITER", "SC_CLAIM", "SC_JIT", "SC_NEED", "SC_REJ", "SC_CAM", "SC_SCAT", "SC_HIT", "SC_SKY", "SC_SHADE",
-           "SC_END"]
+REGIONS = ["SC_ITER", "SC_CLAIM", "SC_SETUP", "SC_PHASE", "SC_JIT", "SC_LENS", "SC_CAM", "SC_TAKE", "SC_NEED", "SC_REJ",
+           "SC_SCAT", "SC_HIT", "SC_SKY", "SC_SHADE", "SC_END"]
 # marker-only regions: the counted region whose entries they share
-DERIVED = {"SC_SETUP": "SC_CLAIM", "SC_ACC": "SC_NEED", "SC_POSTHIT": "SC_HIT", "SC_POSTSHADE": "SC_ITER",
-           "SC_LATCH": "SC_ITER"}
+DERIVED = {"SC_ACC": "SC_NEED", "SC_POSTHIT": "SC_HIT", "SC_POSTSHADE": "SC_ITER", "SC_LATCH": "SC_ITER"}
 # render.hip jit_defines() for the default build
 DEFINES = dict(FR_KREJ=4, FR_KREJ_NIB=9, FR_CLAIM_MIN=1, FR_CLAIM_MIN_NIB=3, FR_NUM_SGPR=96, FR_BLOCK_SAMPLES=16,
-               FR_FINE_SAMPLES=4, FR_STAGE=4, FR_BVH_STAGE=2, FR_NIB_WAVES=8, FR_DIFF12_WAVES=7)
+               FR_FINE_SAMPLES=4, FR_STAGE=4, FR_BVH_STAGE=2, FR_NIB_WAVES=8, FR_DIFF12_WAVES=7, FR_CAMB=1, FR_CAM_MIN=40,
+               FR_KLENS=4)
 OPTS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt",
         "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize"]
 
@@ -73,7 +73,7 @@ def count_regions(asm):
     """VALU / SALU / LDS / memory instructions per region. A marker labels its basic block
     (the assembler comment may sit anywhere in the block); an unmarked block takes the
     region of the block before it in the layout, except: blocks of the rejection loop
-    (the loop nested in the lane loop) are SC_REJ; lane-loop blocks laid out before the
+    (the loops nested in the lane loop) are SC_REJ / SC_LENS; lane-loop blocks laid out before the
     loop header are SC_LATCH; unmarked blocks with a full IEEE division (v_div_fixup: the
     reciprocal guard's fallback) are RARE (not entered in a normal frame); blocks after
     the lane loop are EPILOGUE."""
@@ -113,14 +113,15 @@ def count_regions(asm):
     # the inner loop's header in their comments
     hdr = next(b["name"] for b in blocks if b["mark"] == "SC_ITER")
     lane_loop = "Header=" + hdr.lstrip(".").replace("LBB0_", "BB0_")
-    inner = None
+    inner = {}  # inner loop header -> its region (the blocks of each loop name their header)
     for b in blocks:
-        if b["mark"] == "SC_REJ":
-            inner = b["name"].lstrip(".").replace("LBB0_", "BB0_")
+        if b["mark"] in ("SC_REJ", "SC_LENS"):
+            inner[b["name"].lstrip(".").replace("LBB0_", "BB0_")] = b["mark"]
     region, seen_hdr, done = "PROLOGUE", False, False
     tab = {}
     for b in blocks:
-        in_lane = lane_loop in b["cmt"] or ("Parent Loop " + hdr.lstrip(".").replace("LBB0_", "BB0_")) in b["cmt"]
+        in_lane = lane_loop in b["cmt"] or ("Parent Loop " + hdr.lstrip(".").replace("LBB0_", "BB0_")) in b["cmt"] or (
+            seen_hdr and "Depth=" in b["cmt"])
         if b["name"] == hdr:
             seen_hdr = True
         if b["mark"]:
@@ -130,8 +131,9 @@ def count_regions(asm):
         elif in_lane and not seen_hdr:
             region = "SC_LATCH"
         r = region
-        if inner and ("Header=" + inner) in b["cmt"] and not b["mark"]:
-            r = "SC_REJ"
+        for h, reg in inner.items():
+            if ("Header=" + h + " ") in (b["cmt"] + " ") and not b["mark"]:
+                r = reg
         if not b["mark"] and "v_div_fixup_f32" in b["ops"] and r not in ("SC_SKY",):
             r = "RARE"
         t = tab.setdefault(r, {"valu": 0, "salu": 0, "lds": 0, "mem": 0, "blocks": 0})
