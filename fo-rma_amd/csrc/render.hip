@@ -516,6 +516,8 @@ static std::string jit_defines() {
   def("FR_CAMB", FR_CAMB);
   def("FR_CAM_MIN", FR_CAM_MIN);
   def("FR_KLENS", FR_KLENS);
+  def("FR_RECB", FR_RECB);
+  def("FR_URG_MIN", FR_URG_MIN);
   def("FR_BVH_STAGE", FR_BVH_STAGE);
 #ifdef FR_TRACE_PRIO
   def("FR_TRACE_PRIO", FR_TRACE_PRIO);
@@ -976,9 +978,11 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   const size_t stage_n = stage_samples(use_bvh);
   // the kernel's camera-batching slots (trace_kernel.h camb_kernel): 24 B per lane
   const bool camb = camb_kernel(nibble ? 2 : defer ? 1 : 0, use_bvh);
+  const bool recb = recb_kernel(nibble ? 2 : defer ? 1 : 0, use_bvh);  // (+ 8 B per lane)
   const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * wps * sizeof(float) : 0u) +
-                     (camb ? kBlock * kCamSlotFloats * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 + n_rec * 64 +
-                     stack_bytes + (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
+                     (camb ? kBlock * kCamSlotFloats * sizeof(float) : 0u) +
+                     (recb ? kBlock * kRecSlotFloats * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
+                     n_rec * 64 + stack_bytes + (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
   // the scene-specialised kernel (jit.h): list-loop scenes of <= kJitMaxPrims primitives,
   // when the caller asks (FR_FLAG_SCENE_JIT; FR_SCENE_JIT=1 / 0 forces it on / off)
   JitReq jr;

@@ -138,6 +138,11 @@ constexpr uint32_t kBatch = 64;
 #ifndef FR_CAM_MIN
 #define FR_CAM_MIN 40
 #endif
+// urgent lanes (a path ended without a prepared ray) wait, idle, until FR_URG_MIN of them
+// need a ray or no lane has other work (tuning only, results unchanged)
+#ifndef FR_URG_MIN
+#define FR_URG_MIN 1
+#endif
 // lens rejection: lanes left to the next phase (tuning only, results unchanged)
 #ifndef FR_KLENS
 #define FR_KLENS 4
@@ -145,6 +150,15 @@ constexpr uint32_t kBatch = 64;
 __host__ __device__ constexpr bool camb_kernel(int defer, bool bvh) {
   return FR_CAMB == 2 ? !bvh : FR_CAMB == 1 ? defer == 2 : false;
 }
+// Record batching (8-B-record kernels with camera batching): a path's end parks its escaping
+// direction's d.y and |d|^2 in an LDS slot (2 floats per lane) and its winners in the
+// staging slot; the sky parameter and the sample's store are made in the next camera phase,
+// several lanes together (or at once, when the item ends or another path ends first).
+#ifndef FR_RECB
+#define FR_RECB 1
+#endif
+__host__ __device__ constexpr bool recb_kernel(int defer, bool bvh) { return FR_RECB && defer == 2 && camb_kernel(defer, bvh); }
+constexpr uint32_t kRecSlotFloats = 2;
 constexpr uint32_t kCamSlotFloats = 6;  // o, d of one prepared camera ray (level-major in LDS)
 
 struct KScene {
@@ -327,8 +341,9 @@ enum { PF_CLAIM, PF_REJ, PF_HIT, PF_SHADE, PF_END, PF_N };
 // The first SC_N regions are counted (counters[4 + k]); the others only mark a boundary in
 // the listing, and their entries follow from a counted one (ACC = NEED, POSTHIT = HIT,
 // POSTSHADE = LATCH = ITER; GRAB = the batches the queue hands out).
-enum { SC_ITER, SC_CLAIM, SC_SETUP, SC_PHASE, SC_JIT, SC_LENS, SC_CAM, SC_TAKE, SC_NEED, SC_REJ, SC_SCAT, SC_HIT,
-       SC_SKY, SC_SHADE, SC_END, SC_N, SC_GRAB = SC_N, SC_ACC, SC_POSTHIT, SC_POSTSHADE, SC_LATCH };
+enum { SC_ITER, SC_CLAIM, SC_SETUP, SC_PHASE, SC_FLUSH, SC_JIT, SC_LENS, SC_CAM, SC_TAKE, SC_NEED, SC_REJ, SC_SCAT,
+       SC_HIT, SC_SKY, SC_SHADE, SC_END, SC_FLUSH2, SC_FLUSHC, SC_N, SC_GRAB = SC_N, SC_ACC, SC_POSTHIT,
+       SC_POSTSHADE, SC_LATCH };
 #if defined(FR_SEC_MARKS) && defined(__HIP_DEVICE_COMPILE__)
 #define SEC(k) asm volatile(";FRSEC " #k)
 #elif defined(FR_SECCNT)
@@ -493,6 +508,7 @@ void trace_kernel(
   constexpr bool DIFFUSE = MAT == 1;           // lambertian scatters only
   constexpr bool SKYD = NIB && kSkyDefer;      // 12-B records {d.y, dot(d, d), winners}
   constexpr bool CAMB = camb_kernel(DEFER, BVH);  // camera batching (prepared rays in LDS)
+  constexpr bool RECB = recb_kernel(DEFER, BVH) && !SKYD;  // record batching (parked records in LDS)
   constexpr uint32_t WPS = NIB && !SKYD ? 2u : 3u;  // words per sample in the buffer
   // list kernels always stage; BVH kernels when the launch gave them the LDS (KF_STAGE)
   constexpr bool RSTG = BVH && FR_BVH_RSTAGE != 0;  // pairs staged in registers
@@ -512,8 +528,11 @@ void trace_kernel(
     __device__ __forceinline__ float& operator[](uint32_t k) const { return p[k * kBlock]; }
   };
   const CamSlot cslot{reinterpret_cast<float*>(lds) + (staged ? kBlock * WPS * STG : 0u) + threadIdx.x};
+  // RECB: the parked record's d.y and |d|^2 (level-major, after the camera slots)
+  const CamSlot pslot{cslot.p + (CAMB ? kBlock * kCamSlotFloats : 0u)};
   float4* att_lds = reinterpret_cast<float4*>(lds + (staged ? kBlock * WPS * STG : 0u) +
-                                              (CAMB ? kBlock * kCamSlotFloats : 0u));
+                                              (CAMB ? kBlock * kCamSlotFloats : 0u) +
+                                              (recb_kernel(DEFER, BVH) ? kBlock * kRecSlotFloats : 0u));
   float4* rec_lds = att_lds + n_att_st;
   uint32_t* stack = reinterpret_cast<uint32_t*>(rec_lds + 4u * n_rec);
   uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
@@ -605,11 +624,42 @@ void trace_kernel(
   // ((u, v) in cslot, or in d.xy without camera batching)
   bool active = true, need_item = true, urgent = false, have_ray = false, need_scat = false;
   bool cam_ready = false, lens_pend = false;
+  bool rec_pend = false;  // RECB: sample jj - 1's record is parked (pslot, winners in the stage)
 
 #ifdef FR_PROF
   uint64_t pf_acc[PF_N] = {0, 0, 0, 0, 0};
   uint64_t pf_t = __builtin_amdgcn_s_memtime();
 #endif
+  // The staged samples of group jr / STG (sample jr the group's last so far) to the item's
+  // slots: whole 16-B stores for a full group of a 16-sample slot, else word by word.
+  auto store_group = [&](uint32_t jr) {
+    float* const out = kw.samples + WPS * (static_cast<size_t>(oitem) * kp.ks);  // the item's first slot
+    float* dst = out + WPS * (jr & ~(STG - 1u));
+    if ((jr & (STG - 1u)) == STG - 1u && kp.ks == kBlockSamples) {
+      if constexpr ((WPS * STG) % 4u == 0u) {
+        // 16-B aligned: item * 192 (128) B + a multiple of 48 (32) B
+        const float4* src = reinterpret_cast<const float4*>(stage);
+#pragma unroll
+        for (uint32_t k = 0; k < WPS * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
+      } else {
+        // 8-B aligned: item * 192 B + a multiple of 24 B
+        const float2* src = reinterpret_cast<const float2*>(stage);
+#pragma unroll
+        for (uint32_t k = 0; k < WPS * STG / 2u; ++k) reinterpret_cast<float2*>(dst)[k] = src[k];
+      }
+    } else {
+      for (uint32_t k = 0; k < WPS * ((jr & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
+    }
+  };
+  // RECB: sample jr's parked record to its staging slot (the sky parameter of tracer.rs:211-218
+  // from d.y and |d|^2 by sky_t(d)'s own operations, or the absorbed marker), and the group
+  // out when it is complete or jr is the item's last sample
+  auto flush = [&](uint32_t jr) {
+    const uint32_t ddb = __float_as_uint(pslot[1]);
+    const uint32_t t = ddb == kDeferAbsorbed ? kDeferAbsorbed : __float_as_uint(sky_t_from(pslot[0], __uint_as_float(ddb)));
+    stage[WPS * (jr & (STG - 1u))] = __uint_as_float(t);
+    if ((jr & (STG - 1u)) == STG - 1u || jr + 1u == jend) store_group(jr);
+  };
   // the wave's claimed item batch [q_next, q_end): wave-uniform, updated only under
   // the uniform branch below, so it lives in scalar registers
   uint32_t q_next = 0, q_end = 0;
@@ -718,6 +768,7 @@ void trace_kernel(
       q_next = grab ? base + (n - avail) : next + n;
       const uint32_t item = r < avail ? next + r : base + (r - avail);
       if (need_item && item >= kp.n_items) {
+        if (RECB && rec_pend) flush(jj - 1u);  // the lane's last record
 #ifdef FR_DIAG
         if (gw < 65536) {
           const unsigned long long now = __builtin_amdgcn_s_memrealtime();
@@ -739,6 +790,11 @@ void trace_kernel(
           ok = ok && kp.band_h && y / kp.band_h < 4u;
         }
         if (ok) {
+          if (RECB && rec_pend) {
+            SEC(SC_FLUSHC);
+            flush(jj - 1u);  // the old item's last record, before its slots change
+            rec_pend = false;
+          }
           rng = st;  // this item's streams: rng_seed2(seed, y * W + x, stream_key(b))
           crng = ct;
           // a sub-block k of block b_fine: samples [16 b + 4 k, +4) of the block's slot
@@ -768,8 +824,16 @@ void trace_kernel(
     // fraction of the iterations at several times the width. The camera stream makes the
     // next sample's ray independent of this sample's scatter draws (rt_core.h).
     const bool want = CAMB ? (!need_item && !cam_ready && (urgent || jj + 1u < jend)) : urgent;
-    if (__ballot(urgent) != 0 || (CAMB && lanes_set(want) >= static_cast<uint32_t>(FR_CAM_MIN))) {
+    const unsigned long long murg = __ballot(urgent);
+    constexpr uint32_t URG_MIN = CAMB ? FR_URG_MIN : 1u;
+    if ((murg != 0 && (URG_MIN <= 1 || lanes_set(urgent) >= URG_MIN || __ballot(have_ray || need_scat) == 0)) ||
+        (CAMB && lanes_set(want) >= static_cast<uint32_t>(FR_CAM_MIN))) {
       SEC(SC_PHASE);
+      if (RECB && rec_pend) {
+        SEC(SC_FLUSH);
+        flush(jj - 1u);  // the record parked at the last path end
+        rec_pend = false;
+      }
       if (want) {
         float u, v;
         if (lens_pend) {
@@ -1193,7 +1257,7 @@ void trace_kernel(
       SEC(SC_POSTHIT);
       if (best < 0) {
         SEC(SC_SKY);
-        if (SKYD) {
+        if (SKYD || RECB) {
           sky_dy = d.y;
           tsky = __float_as_uint(d.x * d.x + d.y * d.y + d.z * d.z);  // length()'s sum, in its order
         } else if (DEFER)
@@ -1289,7 +1353,20 @@ void trace_kernel(
       DIAG_WAVE(DG_END_W);
       DIAG_LANE(DG_END_L);
       V3 col = term;
-      if (SKYD) {
+      if (RECB) {
+        // park the record: an earlier parked one goes out first (its path ended before a
+        // phase took it). The item's last one stays parked too: the next phase, or the
+        // lane's next claim (before the item changes), sends it out.
+        if (rec_pend) {
+          SEC(SC_FLUSH2);
+          flush(jj - 1u);
+        }
+        pslot[0] = sky_dy;
+        pslot[1] = __uint_as_float(tsky);  // |d|^2, or the absorbed marker
+        stage[WPS * (jj & (STG - 1u)) + 1u] = __uint_as_float(wnib);
+        wnib = ~0u;  // the next sample starts empty
+        rec_pend = true;
+      } else if (SKYD) {
         col = V3{sky_dy, __uint_as_float(tsky), __uint_as_float(wnib)};
         wnib = ~0u;  // the next sample starts empty
       } else if (NIB) {
@@ -1336,7 +1413,9 @@ void trace_kernel(
       }
       // the item's first sample slot (item-major buffer)
       float* const out = kw.samples + WPS * (static_cast<size_t>(oitem) * kp.ks);
-      if (RSTG) {
+      if (RECB) {
+        // (parked above)
+      } else if (RSTG) {
         // pairs start on even jj (blocks and sub-blocks do): the odd sample stores both
         if (jj & 1u) {
           float* dst = out + WPS * (jj - 1u);
@@ -1375,25 +1454,7 @@ void trace_kernel(
         sl[0] = col.x;
         sl[1] = col.y;
         if (WPS == 3) sl[2] = col.z;
-        const bool full = (jj & (STG - 1u)) == STG - 1u;
-        if (full || jj + 1u == jend) {
-          float* dst = out + WPS * (jj & ~(STG - 1u));
-          if (full && kp.ks == kBlockSamples) {
-            if constexpr ((WPS * STG) % 4u == 0u) {
-              // 16-B aligned: item * 192 (128) B + a multiple of 48 (32) B
-              const float4* src = reinterpret_cast<const float4*>(stage);
-#pragma unroll
-              for (uint32_t k = 0; k < WPS * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
-            } else {
-              // 8-B aligned: item * 192 B + a multiple of 24 B
-              const float2* src = reinterpret_cast<const float2*>(stage);
-#pragma unroll
-              for (uint32_t k = 0; k < WPS * STG / 2u; ++k) reinterpret_cast<float2*>(dst)[k] = src[k];
-            }
-          } else {
-            for (uint32_t k = 0; k < WPS * ((jj & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
-          }
-        }
+        if ((jj & (STG - 1u)) == STG - 1u || jj + 1u == jend) store_group(jj);
       }
       ++jj;
 #ifdef FR_DIAG

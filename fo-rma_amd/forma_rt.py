@@ -168,7 +168,8 @@ def lib():
     L.fr_render_hip_multi.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
     L.fr_selftest_ops.argtypes = [C.c_int, C.c_int, f3, f3, C.c_uint32, f3]
     L.fr_selftest_rng.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
-    L.fr_selftest_rng_camera.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
+    if hasattr(L, "fr_selftest_rng_camera"):  # (A/B builds of earlier revisions lack it)
+        L.fr_selftest_rng_camera.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
     if hasattr(L, "fr_post_process"):  # absent from A/B builds of older sources
         L.fr_post_process.argtypes = [C.c_int, P(C.c_int), C.c_uint32, C.c_float, C.c_uint32, C.c_uint32,
                                       P(C.c_uint8), P(C.c_uint8)]

@@ -24,8 +24,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "fo-rma_amd", "csrc")
 # counted regions, in trace_kernel.h's SC_* order
-REGIONS = ["SC_ITER", "SC_CLAIM", "SC_SETUP", "SC_PHASE", "SC_JIT", "SC_LENS", "SC_CAM", "SC_TAKE", "SC_NEED", "SC_REJ",
-           "SC_SCAT", "SC_HIT", "SC_SKY", "SC_SHADE", "SC_END"]
+REGIONS = ["SC_ITER", "SC_CLAIM", "SC_SETUP", "SC_PHASE", "SC_FLUSH", "SC_JIT", "SC_LENS", "SC_CAM", "SC_TAKE", "SC_NEED",
+           "SC_REJ", "SC_SCAT", "SC_HIT", "SC_SKY", "SC_SHADE", "SC_END", "SC_FLUSH2", "SC_FLUSHC"]
 # marker-only regions: the counted region whose entries they share
 DERIVED = {"SC_ACC": "SC_NEED", "SC_POSTHIT": "SC_HIT", "SC_POSTSHADE": "SC_ITER", "SC_LATCH": "SC_ITER"}
 # render.hip jit_defines() for the default build
