@@ -197,12 +197,9 @@ __global__ void recip_check_kernel(uint64_t base, uint64_t count, unsigned long 
   }
 }
 
-// the trace kernel's seeding (rng_seed2): the scatter stream, or with camera the camera stream
-__global__ void rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out, int camera) {
+__global__ void rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  Rng sr, cr;
-  rng_seed2(seed, pixel, sample, sr, cr);
-  Rng r = camera ? cr : sr;
+  Rng r = rng_seed(seed, pixel, sample);
   for (uint32_t i = 0; i < n; ++i) out[i] = rng_next(r);
 }
 
@@ -513,11 +510,6 @@ static std::string jit_defines() {
   def("FR_BLOCK_SAMPLES", FR_BLOCK_SAMPLES);
   def("FR_FINE_SAMPLES", FR_FINE_SAMPLES);
   def("FR_STAGE", FR_STAGE);
-  def("FR_CAMB", FR_CAMB);
-  def("FR_CAM_MIN", FR_CAM_MIN);
-  def("FR_KLENS", FR_KLENS);
-  def("FR_RECB", FR_RECB);
-  def("FR_URG_MIN", FR_URG_MIN);
   def("FR_BVH_STAGE", FR_BVH_STAGE);
 #ifdef FR_TRACE_PRIO
   def("FR_TRACE_PRIO", FR_TRACE_PRIO);
@@ -976,12 +968,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
                                                sizeof(uint32_t);
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
   const size_t stage_n = stage_samples(use_bvh);
-  // the kernel's camera-batching slots (trace_kernel.h camb_kernel): 24 B per lane
-  const bool camb = camb_kernel(nibble ? 2 : defer ? 1 : 0, use_bvh);
-  const bool recb = recb_kernel(nibble ? 2 : defer ? 1 : 0, use_bvh);  // (+ 8 B per lane)
-  const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * wps * sizeof(float) : 0u) +
-                     (camb ? kBlock * kCamSlotFloats * sizeof(float) : 0u) +
-                     (recb ? kBlock * kRecSlotFloats * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
+  const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * wps * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
                      n_rec * 64 + stack_bytes + (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
   // the scene-specialised kernel (jit.h): list-loop scenes of <= kJitMaxPrims primitives,
   // when the caller asks (FR_FLAG_SCENE_JIT; FR_SCENE_JIT=1 / 0 forces it on / off)
@@ -1614,25 +1601,16 @@ int fr_selftest_ops(int device, int op, const float* a, const float* b, uint32_t
   return FR_OK;
 }
 
-static int selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out,
-                        int camera) {
+int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
   if (!out) return set_error(FR_EARG, "fr_selftest_rng: null buffer");
   SET_DEVICE(device);
   uint32_t* d = nullptr;
   HIPCHK(hipMalloc(&d, (n ? n : 1) * sizeof(uint32_t)));
-  hipLaunchKernelGGL(rng_kernel, dim3(1), dim3(64), 0, 0, seed, pixel, sample, n, d, camera);
+  hipLaunchKernelGGL(rng_kernel, dim3(1), dim3(64), 0, 0, seed, pixel, sample, n, d);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(out, d, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIPCHK(hipFree(d));
   return FR_OK;
-}
-
-int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
-  return selftest_rng(device, seed, pixel, sample, n, out, 0);
-}
-
-int fr_selftest_rng_camera(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
-  return selftest_rng(device, seed, pixel, sample, n, out, 1);
 }
 
 /* Diagnostic: exhaustive recip_nr check over [base, base + count) bit patterns;

@@ -67,17 +67,12 @@ FR_HD float schlick(float cosine, float ref_idx) {
 }
 
 // ---------------------------------------------------------------------------
-// RNG. Two streams per (seed, pixel, key): key b for block b of 16 samples, and, when
+// RNG. One stream per (seed, pixel, key): key b for block b of 16 samples, and, when
 // spp > 16, 2^31 | s / 4 for the 4-sample sub-blocks of the pixel's last block
-// (trace_kernel.h stream_key). splitmix64 on x = seed ^ (pixel << 32 | key) gives four
-// outputs: the first two key the scatter stream, the next two the camera stream, each a
-// xoshiro128+ 1.0 state (Blackman & Vigna's generator for floating-point output: only the
-// upper bits are used). The camera stream serves the samples' jitter and lens draws
-// (tracer.rs:171-172, camera.rs:62-72) in sample order; the scatter stream their scatter
-// draws (sphere.rs / plane.rs scatter) in sample order. The reference draws everything
-// from one sequential ThreadRng (tracer.rs:164-175); with the camera draws on their own
-// stream, the next sample's camera ray does not wait for this sample's last scatter.
-// f32 = ((u32 ^ 2^31) >> 8) * 2^-24.
+// (render.hip stream_key). splitmix64 keys a xoshiro128+ 1.0 state (Blackman & Vigna's
+// generator for floating-point output: only the upper bits are used); a stream's
+// samples draw from it in sample order (the reference's save_image draws every sample
+// from one sequential stream, tracer.rs:164-175). f32 = ((u32 ^ 2^31) >> 8) * 2^-24.
 // ---------------------------------------------------------------------------
 struct Rng {
   uint32_t s0, s1, s2, s3;
@@ -97,19 +92,6 @@ FR_HD Rng rng_seed(uint64_t seed, uint32_t pixel, uint32_t block) {
   uint64_t b = splitmix64_next(x);
   return Rng{static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
              static_cast<uint32_t>(b >> 32)};
-}
-
-// both streams of (seed, pixel, key): splitmix64 outputs 1-2 (scatter) and 3-4 (camera)
-FR_HD void rng_seed2(uint64_t seed, uint32_t pixel, uint32_t block, Rng& scatter, Rng& camera) {
-  uint64_t x = seed ^ ((static_cast<uint64_t>(pixel) << 32) | static_cast<uint64_t>(block));
-  const uint64_t a = splitmix64_next(x);
-  const uint64_t b = splitmix64_next(x);
-  const uint64_t c = splitmix64_next(x);
-  const uint64_t e = splitmix64_next(x);
-  scatter = Rng{static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
-                static_cast<uint32_t>(b >> 32)};
-  camera = Rng{static_cast<uint32_t>(c), static_cast<uint32_t>(c >> 32), static_cast<uint32_t>(e),
-               static_cast<uint32_t>(e >> 32)};
 }
 
 FR_HD uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }

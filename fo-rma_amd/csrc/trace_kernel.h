@@ -127,40 +127,6 @@ static_assert(kFineSamples >= 1 && kBlockSamples % kFineSamples == 0 && kFineSub
 // seeded by the wave's 64 lanes at once (trace_kernel's claim step)
 constexpr uint32_t kBatch = 64;
 
-// Camera batching (the lane loop's camera phase): with CAMB a lane makes the next sample's
-// camera ray while it traces the current one, in a phase several lanes share, and keeps it
-// in an LDS slot (6 floats per lane); without it a lane makes its ray when it needs it.
-// FR_CAMB: 0 never, 1 the 8-B-record kernels (the headline's), 2 every list kernel.
-#ifndef FR_CAMB
-#define FR_CAMB 1
-#endif
-// the phase runs when at least FR_CAM_MIN lanes want a ray (or any lane needs one now)
-#ifndef FR_CAM_MIN
-#define FR_CAM_MIN 40
-#endif
-// urgent lanes (a path ended without a prepared ray) wait, idle, until FR_URG_MIN of them
-// need a ray or no lane has other work (tuning only, results unchanged)
-#ifndef FR_URG_MIN
-#define FR_URG_MIN 1
-#endif
-// lens rejection: lanes left to the next phase (tuning only, results unchanged)
-#ifndef FR_KLENS
-#define FR_KLENS 4
-#endif
-__host__ __device__ constexpr bool camb_kernel(int defer, bool bvh) {
-  return FR_CAMB == 2 ? !bvh : FR_CAMB == 1 ? defer == 2 : false;
-}
-// Record batching (8-B-record kernels with camera batching): a path's end parks its escaping
-// direction's d.y and |d|^2 in an LDS slot (2 floats per lane) and its winners in the
-// staging slot; the sky parameter and the sample's store are made in the next camera phase,
-// several lanes together (or at once, when the item ends or another path ends first).
-#ifndef FR_RECB
-#define FR_RECB 1
-#endif
-__host__ __device__ constexpr bool recb_kernel(int defer, bool bvh) { return FR_RECB && defer == 2 && camb_kernel(defer, bvh); }
-constexpr uint32_t kRecSlotFloats = 2;
-constexpr uint32_t kCamSlotFloats = 6;  // o, d of one prepared camera ray (level-major in LDS)
-
 struct KScene {
   // one 64-B record per primitive (g0..g3; kind in the bits of g3.w): one scalar
   // load brings a primitive into SGPRs in the closest-hit loop
@@ -338,12 +304,11 @@ enum { PF_CLAIM, PF_REJ, PF_HIT, PF_SHADE, PF_END, PF_N };
 //   FR_SECCNT:    SEC(k) counts the wave-level entries of region k (first active lane, an LDS
 //                 add; per launch into counters[4 + k]) (dynamic).
 // Static VALU per region x wave entries per region = the launch's VALU instructions by phase.
-// The first SC_N regions are counted (counters[4 + k]); the others only mark a boundary in
-// the listing, and their entries follow from a counted one (ACC = NEED, POSTHIT = HIT,
+// The first SC_N regions are counted; the others only mark a boundary in the listing, and
+// their entries follow from a counted one (SETUP ~ CLAIM, ACC = NEED, POSTHIT = HIT,
 // POSTSHADE = LATCH = ITER; GRAB = the batches the queue hands out).
-enum { SC_ITER, SC_CLAIM, SC_SETUP, SC_PHASE, SC_FLUSH, SC_JIT, SC_LENS, SC_CAM, SC_TAKE, SC_NEED, SC_REJ, SC_SCAT,
-       SC_HIT, SC_SKY, SC_SHADE, SC_END, SC_FLUSH2, SC_FLUSHC, SC_N, SC_GRAB = SC_N, SC_ACC, SC_POSTHIT,
-       SC_POSTSHADE, SC_LATCH };
+enum { SC_ITER, SC_CLAIM, SC_JIT, SC_NEED, SC_REJ, SC_CAM, SC_SCAT, SC_HIT, SC_SKY, SC_SHADE, SC_END, SC_N,
+       SC_GRAB = SC_N, SC_SETUP, SC_ACC, SC_POSTHIT, SC_POSTSHADE, SC_LATCH };
 #if defined(FR_SEC_MARKS) && defined(__HIP_DEVICE_COMPILE__)
 #define SEC(k) asm volatile(";FRSEC " #k)
 #elif defined(FR_SECCNT)
@@ -482,8 +447,7 @@ template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, int DEF
 #define FR_OCC_ATTR \
   __attribute__((amdgpu_waves_per_eu(BVH ? 6 : DEFER == 2 ? FR_NIB_WAVES : (DEFER == 1 && MAT == 1) ? FR_DIFF12_WAVES : 7)))
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) FR_OCC_ATTR
-void trace_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) FR_OCC_ATTR void trace_kernel(
     KArgs args) {
   // one by-value struct: the kernarg segment holds it at offset 0 (the camera is read
   // back from there in the lens step)
@@ -507,8 +471,6 @@ void trace_kernel(
   constexpr bool NIB = DEFER == 2;             // 8-B records, winners in a register
   constexpr bool DIFFUSE = MAT == 1;           // lambertian scatters only
   constexpr bool SKYD = NIB && kSkyDefer;      // 12-B records {d.y, dot(d, d), winners}
-  constexpr bool CAMB = camb_kernel(DEFER, BVH);  // camera batching (prepared rays in LDS)
-  constexpr bool RECB = recb_kernel(DEFER, BVH) && !SKYD;  // record batching (parked records in LDS)
   constexpr uint32_t WPS = NIB && !SKYD ? 2u : 3u;  // words per sample in the buffer
   // list kernels always stage; BVH kernels when the launch gave them the LDS (KF_STAGE)
   constexpr bool RSTG = BVH && FR_BVH_RSTAGE != 0;  // pairs staged in registers
@@ -522,17 +484,7 @@ void trace_kernel(
   const uint32_t n_att = ATT_LDS || sc.n <= kAttLds ? sc.n : 0u;
   const uint32_t n_att_st = n_att ? n_att + 1u : 0u;  // with the unit entry
   const uint32_t n_rec = REC_LDS || sc.n <= kRecLds ? sc.n : 0u;
-  // CAMB: the prepared camera rays, level-major (float k of lane t at cslot[k * kBlock])
-  struct CamSlot {
-    float* p;
-    __device__ __forceinline__ float& operator[](uint32_t k) const { return p[k * kBlock]; }
-  };
-  const CamSlot cslot{reinterpret_cast<float*>(lds) + (staged ? kBlock * WPS * STG : 0u) + threadIdx.x};
-  // RECB: the parked record's d.y and |d|^2 (level-major, after the camera slots)
-  const CamSlot pslot{cslot.p + (CAMB ? kBlock * kCamSlotFloats : 0u)};
-  float4* att_lds = reinterpret_cast<float4*>(lds + (staged ? kBlock * WPS * STG : 0u) +
-                                              (CAMB ? kBlock * kCamSlotFloats : 0u) +
-                                              (recb_kernel(DEFER, BVH) ? kBlock * kRecSlotFloats : 0u));
+  float4* att_lds = reinterpret_cast<float4*>(lds + (staged ? kBlock * WPS * STG : 0u));
   float4* rec_lds = att_lds + n_att_st;
   uint32_t* stack = reinterpret_cast<uint32_t*>(rec_lds + 4u * n_rec);
   uint16_t* hstack = reinterpret_cast<uint16_t*>(stack);
@@ -578,12 +530,13 @@ void trace_kernel(
 
   const float fW = static_cast<float>(kp.W), fH = static_cast<float>(kp.H);
 
+  enum : uint32_t { NEED_NONE = 0, NEED_LENS = 1, NEED_SPHERE = 2 };
   uint32_t depth = 0;  // scatters of the path (not NIB: wnib holds them)
-  // NIB: the winners as 4-bit entries, the last one pushed in bits 28..31 and the first
-  // in bits 32 - 4 depth .. 35 - 4 depth, 15 on the levels below (empty): sum_kernel
-  // multiplies nibble 7 first, so the path's winners are applied innermost first and the
-  // empty levels' unit entries last (x * 1 = x). With d pushes nibble 8 - d is the first
-  // empty one: depth < max_depth iff the nibbles under dmask are still empty.
+  // NIB: the winners as 4-bit entries, the last one pushed in bits 28..31 and the first in
+  // bits 32 - 4 depth .. 35 - 4 depth, 15 on the levels below (empty). sum_kernel multiplies
+  // nibble 7 first, so the path's winners are applied innermost first and the empty levels'
+  // unit entries last (x * 1 = x). With d pushes nibble 8 - d is the first empty one:
+  // depth < max_depth iff the nibbles under dmask are still empty.
   uint32_t wnib = ~0u;
   const uint32_t dmask = kp.max_depth ? (0xFu << (4u * (8u - min(kp.max_depth, 8u)))) : 0u;
   // stack push at level `depth` of the scatter winner
@@ -598,76 +551,36 @@ void trace_kernel(
       stack[depth * kBlock + tid] = pi;
   };
 
-  // the ray; while a scatter sample is pending o = hit point and d = scatter base
-  // ((p + n), or reflect(unit(d), n) for metal); without camera batching, while an urgent
-  // lane's lens sample is pending d.xy = (u, v)
+  // the ray; while a lens sample is pending d.xy = (u, v); while a scatter sample is
+  // pending o = hit point and d = scatter base ((p + n), or reflect(unit(d), n) for metal)
   V3 o{0.0f, 0.0f, 0.0f}, d{0.0f, 0.0f, 1.0f};
   V3 sn{0.0f, 0.0f, 0.0f};  // metal: normal
-  float sfuzz = 0.0f;
+  float sfuzz = 0.0f, fx = 0.0f, fy = 0.0f, vofs = 0.0f;
   bool smetal = false;
-  uint32_t sbest = 0, nseg = 0, nhit = 0;  // (scatters = segments - samples: the host's)
-  // sample jj of the item's block is traced (or, for an urgent lane, needs its camera ray);
-  // jend: one past the item's last sample; xy: the item's pixel (x | y << 16); oitem: the
-  // item's slot run in the sample buffer (item - k P for sub-block k)
-  uint32_t jj = 0, jend = 0, xy = 0, oitem = 0;
+  uint32_t sbest = 0, s = 0, s_end = 0, nseg = 0, nhit = 0;  // (scatters = segments - samples: the host's)
+  uint32_t jj = 0;           // sample index within the item's block
   V3 pend{0.0f, 0.0f, 0.0f};  // RSTG: the pair's first colour (an even jj)
 #ifdef FR_DIAG
   uint32_t diag_tb = 0, diag_seg0 = 0;  // the item's batch index, segments at its claim
   uint32_t diag_iter = 0;               // loop iterations of this wave
 #endif
-  Rng rng{0u, 0u, 0u, 0u};   // the item's scatter stream
-  Rng crng{0u, 0u, 0u, 0u};  // the item's camera stream (jitter and lens draws)
-  // need_item: the lane has no item; urgent: it needs its camera ray to trace (a claimed
-  // item's first sample, or a path ended without a prepared ray); need_scat: a scatter
-  // sample (rejection) is pending; cam_ready (CAMB): cslot holds the next sample's camera
-  // ray; lens_pend: the camera ray being made has its jitter, its lens sample is pending
-  // ((u, v) in cslot, or in d.xy without camera batching)
-  bool active = true, need_item = true, urgent = false, have_ray = false, need_scat = false;
-  bool cam_ready = false, lens_pend = false;
-  bool rec_pend = false;  // RECB: sample jj - 1's record is parked (pslot, winners in the stage)
+  float* out = kw.samples;   // the item's first sample slot (item-major buffer)
+  Rng rng{0u, 0u, 0u, 0u};
+  bool active = true, need_item = true, need_jit = false, have_ray = false;
+  uint32_t need = NEED_NONE;
 
 #ifdef FR_PROF
   uint64_t pf_acc[PF_N] = {0, 0, 0, 0, 0};
   uint64_t pf_t = __builtin_amdgcn_s_memtime();
 #endif
-  // The staged samples of group jr / STG (sample jr the group's last so far) to the item's
-  // slots: whole 16-B stores for a full group of a 16-sample slot, else word by word.
-  auto store_group = [&](uint32_t jr) {
-    float* const out = kw.samples + WPS * (static_cast<size_t>(oitem) * kp.ks);  // the item's first slot
-    float* dst = out + WPS * (jr & ~(STG - 1u));
-    if ((jr & (STG - 1u)) == STG - 1u && kp.ks == kBlockSamples) {
-      if constexpr ((WPS * STG) % 4u == 0u) {
-        // 16-B aligned: item * 192 (128) B + a multiple of 48 (32) B
-        const float4* src = reinterpret_cast<const float4*>(stage);
-#pragma unroll
-        for (uint32_t k = 0; k < WPS * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
-      } else {
-        // 8-B aligned: item * 192 B + a multiple of 24 B
-        const float2* src = reinterpret_cast<const float2*>(stage);
-#pragma unroll
-        for (uint32_t k = 0; k < WPS * STG / 2u; ++k) reinterpret_cast<float2*>(dst)[k] = src[k];
-      }
-    } else {
-      for (uint32_t k = 0; k < WPS * ((jr & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
-    }
-  };
-  // RECB: sample jr's parked record to its staging slot (the sky parameter of tracer.rs:211-218
-  // from d.y and |d|^2 by sky_t(d)'s own operations, or the absorbed marker), and the group
-  // out when it is complete or jr is the item's last sample
-  auto flush = [&](uint32_t jr) {
-    const uint32_t ddb = __float_as_uint(pslot[1]);
-    const uint32_t t = ddb == kDeferAbsorbed ? kDeferAbsorbed : __float_as_uint(sky_t_from(pslot[0], __uint_as_float(ddb)));
-    stage[WPS * (jr & (STG - 1u))] = __uint_as_float(t);
-    if ((jr & (STG - 1u)) == STG - 1u || jr + 1u == jend) store_group(jr);
-  };
   // the wave's claimed item batch [q_next, q_end): wave-uniform, updated only under
   // the uniform branch below, so it lives in scalar registers
   uint32_t q_next = 0, q_end = 0;
   // Stream starts of the wave's batch: lane k holds item (batch base + k)'s. The whole
-  // wave seeds a batch when it reserves one, so rng_seed2 (splitmix64: 64-bit multiplies)
-  // runs once per 64 items at full width instead of in every iteration in which a lane or
-  // two claim; a claiming lane fetches its streams by lane permutes.
-  Rng held{0u, 0u, 0u, 0u}, held_c{0u, 0u, 0u, 0u};
+  // wave seeds a batch when it reserves one, so rng_seed (16 quarter-rate 32-bit
+  // multiplies) runs once per 64 items at full width instead of in every iteration in
+  // which a lane or two claim; a claiming lane fetches its stream by a lane permute.
+  Rng held{0u, 0u, 0u, 0u};
   // ... and the same slot's pixel (x | y << 16, all ones past the image edge) and sample
   // block, so a claiming lane fetches those by permute too instead of dividing the item
   uint32_t held_xy = 0xFFFFFFFFu, held_b = 0u;
@@ -687,7 +600,7 @@ void trace_kernel(
     q_end = q_next + kBatch;
     uint32_t bb, qq, xx, yy;
     const bool in_image = item_xy(k0, q_next + lane, bb, qq, xx, yy);
-    rng_seed2(k0.seed, yy * k0.W + xx, stream_key(bb), held, held_c);
+    held = rng_seed(k0.seed, yy * k0.W + xx, stream_key(bb));
     held_xy = in_image ? (xx | (yy << 16)) : 0xFFFFFFFFu;
     held_b = bb;
   }
@@ -719,17 +632,18 @@ void trace_kernel(
       uint32_t base = 0;
       const bool grab = n > avail;
       const int first = __ffsll(static_cast<long long>(m)) - 1;
-      // The item's streams, pixel and block, by lane permute from the lane that seeded
-      // them: first from the current batch (claims r < avail), then, after a grab, from the
-      // new batch (claims r >= avail). Every lane of the wave is active at both permutes (a
-      // permute reads 0 from an inactive source): a lane retires only after the queue has
-      // drained, and from then on no batch holds a valid item.
+      // The item's stream start, pixel and block, by lane permute from the lane that
+      // seeded them: first from the current batch (claims r < avail), then, after a grab,
+      // from the new batch (claims r >= avail). Every lane of the wave is active at both
+      // permutes (a permute reads 0 from an inactive source): a lane retires only after
+      // the queue has drained, and from then on no batch holds a valid item.
       int sl = static_cast<int>(((next + r) & (kBatch - 1u)) << 2);
-      auto perm = [&](uint32_t v) { return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(v))); };
-      Rng st{perm(held.s0), perm(held.s1), perm(held.s2), perm(held.s3)};
-      Rng ct{perm(held_c.s0), perm(held_c.s1), perm(held_c.s2), perm(held_c.s3)};
-      uint32_t cxy = perm(held_xy);
-      uint32_t b = perm(held_b);
+      Rng st{static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s0))),
+             static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s1))),
+             static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s2))),
+             static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s3)))};
+      uint32_t xy = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_xy)));
+      uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_b)));
       if (grab) {
         SEC(SC_GRAB);
         if (static_cast<int>(lane) == first) base = atomicAdd(kw.queue, kBatch);
@@ -737,7 +651,7 @@ void trace_kernel(
         // A slot past the image or the queue gets a stream that is never used.
 #if defined(__HIP_DEVICE_COMPILE__)
         // the item split's parameters reloaded from the kernarg segment here (once per 64
-        // items) rather than held in SGPRs across the loop, like the camera (the phase)
+        // items) rather than held in SGPRs across the loop, like the camera (step 1)
         typedef __attribute__((address_space(4))) const KArgs cargs_g;
         cargs_g* apg = (cargs_g*)(__builtin_amdgcn_kernarg_segment_ptr());
         asm volatile("" : "+s"(apg));
@@ -749,26 +663,26 @@ void trace_kernel(
         q_end = base + kBatch;
         uint32_t bb, qq, xx, yy;
         const bool in_image = item_xy(kg, base + lane, bb, qq, xx, yy);
-        rng_seed2(kg.seed, yy * kg.W + xx, stream_key(bb), held, held_c);
+        held = rng_seed(kg.seed, yy * kg.W + xx, stream_key(bb));
         held_xy = in_image ? (xx | (yy << 16)) : 0xFFFFFFFFu;
         held_b = bb;
         // claims r >= avail take the new batch's slots r - avail (base is a multiple of 64)
         sl = static_cast<int>(((r - avail) & (kBatch - 1u)) << 2);
-        const Rng st2{perm(held.s0), perm(held.s1), perm(held.s2), perm(held.s3)};
-        const Rng ct2{perm(held_c.s0), perm(held_c.s1), perm(held_c.s2), perm(held_c.s3)};
-        const uint32_t xy2 = perm(held_xy);
-        const uint32_t b2 = perm(held_b);
+        const Rng st2{static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s0))),
+                      static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s1))),
+                      static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s2))),
+                      static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held.s3)))};
+        const uint32_t xy2 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_xy)));
+        const uint32_t b2 = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(sl, static_cast<int>(held_b)));
         if (r >= avail) {
           st = st2;
-          ct = ct2;
-          cxy = xy2;
+          xy = xy2;
           b = b2;
         }
       }
       q_next = grab ? base + (n - avail) : next + n;
       const uint32_t item = r < avail ? next + r : base + (r - avail);
       if (need_item && item >= kp.n_items) {
-        if (RECB && rec_pend) flush(jj - 1u);  // the lane's last record
 #ifdef FR_DIAG
         if (gw < 65536) {
           const unsigned long long now = __builtin_amdgcn_s_memrealtime();
@@ -783,105 +697,84 @@ void trace_kernel(
       }
       if (need_item) {
         SEC(SC_SETUP);
-        bool ok = cxy != 0xFFFFFFFFu;
+        const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
+        bool ok = xy != 0xFFFFFFFFu;
+        uint32_t yrow = kp.H - y;  // tracer.rs:171-172: v = ((H - y) + r) / H
         if (MT) {
-          // render_mt (tracer.rs:86-103): rows past 4 * t_height are never rendered
-          const uint32_t y = cxy >> 16;
-          ok = ok && kp.band_h && y / kp.band_h < 4u;
+          // render_mt (tracer.rs:86-103): band k from the top is thread t_id = 3 - k;
+          // v = ((t_height - y_band) + r) / H + t_id * 0.25; rows past 4 * t_height unused
+          const uint32_t k = kp.band_h ? y / kp.band_h : 4u;
+          ok = ok && k < 4u;
+          yrow = kp.band_h - (y - k * kp.band_h);
+          vofs = static_cast<float>(3u - k) * 0.25f;
         }
         if (ok) {
-          if (RECB && rec_pend) {
-            SEC(SC_FLUSHC);
-            flush(jj - 1u);  // the old item's last record, before its slots change
-            rec_pend = false;
-          }
-          rng = st;  // this item's streams: rng_seed2(seed, y * W + x, stream_key(b))
-          crng = ct;
+          rng = st;  // this item's stream: rng_seed(seed, y * W + x, stream_key(b))
           // a sub-block k of block b_fine: samples [16 b + 4 k, +4) of the block's slot
           // (item - k * P in the buffer); a whole block: k = 0
           const uint32_t k = (b >> 28) & 3u;
           const bool fine = (b & kFineKey) != 0u;
           jj = k * kFineSamples;
-          const uint32_t s0 = (b & 0x0FFFFFFFu) * kBlockSamples + jj;
-          jend = jj + (min(s0 + (fine ? kFineSamples : kBlockSamples), kp.spp) - s0);
-          oitem = item - k * kp.P;
-          xy = cxy;
+          s = (b & 0x0FFFFFFFu) * kBlockSamples + jj;
+          out = kw.samples + WPS * (static_cast<size_t>(item - k * kp.P) * kp.ks);
 #ifdef FR_DIAG
           diag_tb = item >> 6;
           diag_seg0 = nseg;
 #endif
-          urgent = true;  // its first sample's camera ray is made in this iteration's phase
-          lens_pend = false;
+          s_end = min(s + (fine ? kFineSamples : kBlockSamples), kp.spp);
+          fx = static_cast<float>(x);
+          fy = static_cast<float>(yrow);
+          need_jit = true;
           need_item = false;
         }
       }
     }
-    // 1. the camera phase (Camera::get_ray, camera.rs:62-72, after the jitter of
-    // tracer.rs:171-172): every lane that will need a camera ray makes it here, together.
-    // With camera batching (CAMB) that is each lane whose next sample has no prepared ray
-    // yet, while it traces the current one: the phase runs when an urgent lane needs its
-    // ray now or when at least FR_CAM_MIN lanes want one, so the camera work runs at a
-    // fraction of the iterations at several times the width. The camera stream makes the
-    // next sample's ray independent of this sample's scatter draws (rt_core.h).
-    const bool want = CAMB ? (!need_item && !cam_ready && (urgent || jj + 1u < jend)) : urgent;
-    const unsigned long long murg = __ballot(urgent);
-    constexpr uint32_t URG_MIN = CAMB ? FR_URG_MIN : 1u;
-    if ((murg != 0 && (URG_MIN <= 1 || lanes_set(urgent) >= URG_MIN || __ballot(have_ray || need_scat) == 0)) ||
-        (CAMB && lanes_set(want) >= static_cast<uint32_t>(FR_CAM_MIN))) {
-      SEC(SC_PHASE);
-      if (RECB && rec_pend) {
-        SEC(SC_FLUSH);
-        flush(jj - 1u);  // the record parked at the last path end
-        rec_pend = false;
-      }
-      if (want) {
-        float u, v;
-        if (lens_pend) {
-          if (CAMB) {
-            u = cslot[0];
-            v = cslot[1];
-          } else {
-            u = d.x;
-            v = d.y;
-          }
-        } else {
-          SEC(SC_JIT);
-          // a sample starts: jitter (tracer.rs:171-172)
-          const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
-          uint32_t yrow = kp.H - y;  // v = ((H - y) + r) / H
-          float vofs = 0.0f;
-          if (MT) {
-            // render_mt (tracer.rs:86-103): band k from the top is thread t_id = 3 - k;
-            // v = ((t_height - y_band) + r) / H + t_id * 0.25
-            const uint32_t k = y / kp.band_h;
-            yrow = kp.band_h - (y - k * kp.band_h);
-            vofs = static_cast<float>(3u - k) * 0.25f;
-          }
-          const float r0 = rng_f32(crng);
-          const float r1 = rng_f32(crng);
-          u = div_rn(static_cast<float>(x) + r0, fW, kp.rW);  // numerator +0 or in [2^-24, 2^32]
-          v = div_rn(static_cast<float>(yrow) + r1, fH, kp.rH);
-          if (MT) v = v + vofs;  // render_mt's band offset (tracer.rs:103)
+    if (need_jit) {
+      SEC(SC_JIT);
+      // a sample starts: jitter (tracer.rs:171-172), then its lens sample in step 1. One
+      // place for the first sample of a block and the next sample of the same block, so
+      // the wave runs it once per iteration
+      const float r0 = rng_f32(rng);
+      const float r1 = rng_f32(rng);
+      d.x = div_rn(fx + r0, fW, kp.rW);  // (fx + r0) / fW, numerator +0 or in [2^-24, 2^32]
+      d.y = div_rn(fy + r1, fH, kp.rH);
+      if (MT) d.y = d.y + vofs;  // render_mt's band offset (tracer.rs:103)
+      need = NEED_LENS;
+      need_jit = false;
+    }
+    PROF_MARK(PF_CLAIM);
+    bool ended = false;
+    V3 term{0.0f, 0.0f, 0.0f};
+    uint32_t tsky = kDeferAbsorbed;  // DEFER: the terminal as sky parameter bits (SKYD: dot(d, d))
+    float sky_dy = 0.0f;             // SKYD: the escaping ray's d.y
+    if (need != NEED_NONE) {
+      SEC(SC_NEED);
+      // 1. merged rejection loop
+      // dd >= 2^46: the lane still rejects (the loop test and the next pass's branch are
+      // one compare on it; a bool carried through the loop cost a select and a compare per
+      // pass to ballot)
+      float px = 0.0f, py = 0.0f, pz = 0.0f, dd = kUnitBallScaled;
+      const bool sph = need == NEED_SPHERE;
+      do {
+        SEC(SC_REJ);
+        DIAG_WAVE(DG_LENS_W);
+        DIAG_LANE(DG_LENS_L);
+        if (dd >= kUnitBallScaled) {
+          // the test in the 2^23-scaled domain (rng_signed_unit_scaled): same decisions
+          px = rng_signed_unit_scaled(rng);
+          py = rng_signed_unit_scaled(rng);
+          if (sph) pz = rng_signed_unit_scaled(rng);  // a circle try keeps pz = 0
+          dd = px * px + py * py + pz * pz;
         }
-        // random_in_unit_circle (utility.rs:4-13) in the 2^23-scaled domain
-        // (rng_signed_unit_scaled: the same decisions as dot(p, p) >= 1). It stops once at
-        // most FR_KLENS lanes still reject; those keep their jitter and camera stream and
-        // go on at the next phase (draws stay in stream order: results do not depend on it)
-        float px = 0.0f, py = 0.0f, dd = kUnitBallScaled;
-        do {
-          SEC(SC_LENS);
-          DIAG_WAVE(DG_LENS_W);
-          DIAG_LANE(DG_LENS_L);
-          if (dd >= kUnitBallScaled) {
-            px = rng_signed_unit_scaled(crng);
-            py = rng_signed_unit_scaled(crng);
-            dd = px * px + py * py;  // + 0 * 0, exact
-          }
-        } while (lanes_set(dd >= kUnitBallScaled) > static_cast<uint32_t>(FR_KLENS));
-        if (dd < kUnitBallScaled) {
+      } while (lanes_set(dd >= kUnitBallScaled) > static_cast<uint32_t>(KREJ));
+      SEC(SC_ACC);
+      if (dd < kUnitBallScaled) {
+        px *= kSignedUnitScale;  // the accepted point, 2r - 1 per coordinate (exact)
+        py *= kSignedUnitScale;
+        pz *= kSignedUnitScale;
+        if (!sph) {
           SEC(SC_CAM);
-          px *= kSignedUnitScale;  // the accepted point, 2r - 1 per coordinate (exact)
-          py *= kSignedUnitScale;
+          // Camera::get_ray (camera.rs:62-72)
 #if !defined(FR_CAM_RESIDENT) && defined(__HIP_DEVICE_COMPILE__)
           // scalar loads of the camera from the kernarg segment, here, rather than 19
           // SGPRs held (and spilled) across the loop: the pointer is opaque to the
@@ -897,90 +790,32 @@ void trace_kernel(
           const V3 cver{cm.vx, cm.vy, cm.vz}, cu{cm.ux, cm.uy, cm.uz}, cv{cm.bx, cm.by, cm.bz};
           const V3 rd = scl(cm.lens, V3{px, py, 0.0f});
           const V3 off = add(scl(rd.x, cu), scl(rd.y, cv));
-          const V3 ro = add(cpos, off);
-          const V3 rdir = sub(sub(add(add(cllc, scl(u, chor)), scl(v, cver)), cpos), off);
-          if (CAMB) {
-            cslot[0] = ro.x;
-            cslot[1] = ro.y;
-            cslot[2] = ro.z;
-            cslot[3] = rdir.x;
-            cslot[4] = rdir.y;
-            cslot[5] = rdir.z;
-            cam_ready = true;
-          } else {
-            o = ro;
-            d = rdir;
-            have_ray = true;
-            urgent = false;
-          }
-          lens_pend = false;
-        } else {
-          // the jitter is drawn; the lens sample goes on at the next phase
-          if (CAMB) {
-            cslot[0] = u;
-            cslot[1] = v;
-          } else {
-            d.x = u;
-            d.y = v;
-          }
-          lens_pend = true;
-        }
-      }
-    }
-    if (CAMB && urgent && cam_ready) {
-      SEC(SC_TAKE);
-      // an urgent lane takes the ray its phase just made
-      o = V3{cslot[0], cslot[1], cslot[2]};
-      d = V3{cslot[3], cslot[4], cslot[5]};
-      cam_ready = false;
-      urgent = false;
-      have_ray = true;
-    }
-    PROF_MARK(PF_CLAIM);
-    bool ended = false;
-    V3 term{0.0f, 0.0f, 0.0f};
-    uint32_t tsky = kDeferAbsorbed;  // DEFER: the terminal as sky parameter bits (SKYD: dot(d, d))
-    float sky_dy = 0.0f;             // SKYD: the escaping ray's d.y
-    if (need_scat) {
-      SEC(SC_NEED);
-      // 2. random_in_unit_sphere (utility.rs:15-25) for the pending scatters, in the
-      // 2^23-scaled domain. It stops once at most KREJ lanes still reject; those keep their
-      // stream and retry next iteration (draws stay in stream order: results do not depend
-      // on KREJ). dd >= 2^46 marks a lane that still rejects (the loop test and the next
-      // pass's branch are one compare)
-      float px = 0.0f, py = 0.0f, pz = 0.0f, dd = kUnitBallScaled;
-      do {
-        SEC(SC_REJ);
-        DIAG_WAVE(DG_RUS_W);
-        DIAG_LANE(DG_RUS_L);
-        if (dd >= kUnitBallScaled) {
-          px = rng_signed_unit_scaled(rng);
-          py = rng_signed_unit_scaled(rng);
-          pz = rng_signed_unit_scaled(rng);
-          dd = px * px + py * py + pz * pz;
-        }
-      } while (lanes_set(dd >= kUnitBallScaled) > static_cast<uint32_t>(KREJ));
-      SEC(SC_ACC);
-      if (dd < kUnitBallScaled) {
-        SEC(SC_SCAT);
-        const V3 r{px * kSignedUnitScale, py * kSignedUnitScale, pz * kSignedUnitScale};  // exact
-        bool ok = true;
-        V3 dir;
-        if (!DIFFUSE && smetal) {
-          dir = add(d, scl(sfuzz, r));  // reflected + fuzz * rus
-          ok = dot(dir, sn) > 0.0f;     // sphere.rs:104 / plane.rs:121
-        } else {
-          dir = sub(add(d, r), o);  // ((p + n) + rus) - p
-        }
-        if (ok) {
-          if (!(NIB && DIFFUSE)) push(sbest);  // (NIB && DIFFUSE kernels pushed at the shading step)
-          if (!NIB) ++depth;
-          d = dir;
+          const float u = d.x, v = d.y;
+          o = add(cpos, off);
+          d = sub(sub(add(add(cllc, scl(u, chor)), scl(v, cver)), cpos), off);
+          if (!NIB) depth = 0;
           have_ray = true;
         } else {
-          ended = true;  // absorbed: get_color returns 0
+          SEC(SC_SCAT);
+          const V3 r{px, py, pz};
+          bool ok = true;
+          V3 dir;
+          if (!DIFFUSE && smetal) {
+            dir = add(d, scl(sfuzz, r));  // reflected + fuzz * rus
+            ok = dot(dir, sn) > 0.0f;     // sphere.rs:104 / plane.rs:121
+          } else {
+            dir = sub(add(d, r), o);  // ((p + n) + rus) - p
+          }
+          if (ok) {
+            if (!(NIB && DIFFUSE)) push(sbest);  // (NIB && DIFFUSE kernels pushed at the shading step)
+            if (!NIB) ++depth;
+            d = dir;
+            have_ray = true;
+          } else {
+            ended = true;  // absorbed: get_color returns 0
+          }
         }
-        need_scat = false;
+        need = NEED_NONE;
       }
     }
     PROF_MARK(PF_REJ);
@@ -1257,7 +1092,7 @@ void trace_kernel(
       SEC(SC_POSTHIT);
       if (best < 0) {
         SEC(SC_SKY);
-        if (SKYD || RECB) {
+        if (SKYD) {
           sky_dy = d.y;
           tsky = __float_as_uint(d.x * d.x + d.y * d.y + d.z * d.z);  // length()'s sum, in its order
         } else if (DEFER)
@@ -1326,7 +1161,7 @@ void trace_kernel(
           sbest = static_cast<uint32_t>(best);
           smetal = !DIFFUSE && c == SC_METAL;
           ended = c == SC_NONE;
-          if (c != SC_NONE && (DIFFUSE || c != SC_DIELECTRIC)) need_scat = true;
+          if (c != SC_NONE && (DIFFUSE || c != SC_DIELECTRIC)) need = NEED_SPHERE;
           // a lambertian scatter always continues the path (sphere.rs:84-89): with only those
           // (and stubs, which end it above) the winner is pushed here, not held to the scatter
           if (NIB && DIFFUSE && c != SC_NONE) push(static_cast<uint32_t>(best));
@@ -1353,20 +1188,7 @@ void trace_kernel(
       DIAG_WAVE(DG_END_W);
       DIAG_LANE(DG_END_L);
       V3 col = term;
-      if (RECB) {
-        // park the record: an earlier parked one goes out first (its path ended before a
-        // phase took it). The item's last one stays parked too: the next phase, or the
-        // lane's next claim (before the item changes), sends it out.
-        if (rec_pend) {
-          SEC(SC_FLUSH2);
-          flush(jj - 1u);
-        }
-        pslot[0] = sky_dy;
-        pslot[1] = __uint_as_float(tsky);  // |d|^2, or the absorbed marker
-        stage[WPS * (jj & (STG - 1u)) + 1u] = __uint_as_float(wnib);
-        wnib = ~0u;  // the next sample starts empty
-        rec_pend = true;
-      } else if (SKYD) {
+      if (SKYD) {
         col = V3{sky_dy, __uint_as_float(tsky), __uint_as_float(wnib)};
         wnib = ~0u;  // the next sample starts empty
       } else if (NIB) {
@@ -1411,11 +1233,7 @@ void trace_kernel(
           for (int j = udepth - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
         }
       }
-      // the item's first sample slot (item-major buffer)
-      float* const out = kw.samples + WPS * (static_cast<size_t>(oitem) * kp.ks);
-      if (RECB) {
-        // (parked above)
-      } else if (RSTG) {
+      if (RSTG) {
         // pairs start on even jj (blocks and sub-blocks do): the odd sample stores both
         if (jj & 1u) {
           float* dst = out + WPS * (jj - 1u);
@@ -1437,7 +1255,7 @@ void trace_kernel(
             dst[WPS + 1] = col.y;
             if (WPS == 3) dst[WPS + 2] = col.z;
           }
-        } else if (jj + 1u == jend) {
+        } else if (s + 1u == s_end) {
           out[WPS * jj] = col.x;
           out[WPS * jj + 1] = col.y;
           if (WPS == 3) out[WPS * jj + 2] = col.z;
@@ -1454,24 +1272,34 @@ void trace_kernel(
         sl[0] = col.x;
         sl[1] = col.y;
         if (WPS == 3) sl[2] = col.z;
-        if ((jj & (STG - 1u)) == STG - 1u || jj + 1u == jend) store_group(jj);
+        const bool full = (jj & (STG - 1u)) == STG - 1u;
+        if (full || s + 1u == s_end) {
+          float* dst = out + WPS * (jj & ~(STG - 1u));
+          if (full && kp.ks == kBlockSamples) {
+            if constexpr ((WPS * STG) % 4u == 0u) {
+              // 16-B aligned: item * 192 (128) B + a multiple of 48 (32) B
+              const float4* src = reinterpret_cast<const float4*>(stage);
+#pragma unroll
+              for (uint32_t k = 0; k < WPS * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
+            } else {
+              // 8-B aligned: item * 192 B + a multiple of 24 B
+              const float2* src = reinterpret_cast<const float2*>(stage);
+#pragma unroll
+              for (uint32_t k = 0; k < WPS * STG / 2u; ++k) reinterpret_cast<float2*>(dst)[k] = src[k];
+            }
+          } else {
+            for (uint32_t k = 0; k < WPS * ((jj & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
+          }
+        }
       }
       ++jj;
 #ifdef FR_DIAG
-      if (jj == jend && diag_tb < (1u << 20)) atomicAdd(&g_fr_tb_cost[diag_tb], nseg - diag_seg0);
+      if (s + 1u == s_end && diag_tb < (1u << 20)) atomicAdd(&g_fr_tb_cost[diag_tb], nseg - diag_seg0);
 #endif
-      if (!NIB) depth = 0;
-      if (jj == jend) {
+      if (++s == s_end)
         need_item = true;
-      } else if (CAMB && cam_ready) {
-        // the next sample of the block (same streams) starts at once on its prepared ray
-        o = V3{cslot[0], cslot[1], cslot[2]};
-        d = V3{cslot[3], cslot[4], cslot[5]};
-        cam_ready = false;
-        have_ray = true;
-      } else {
-        urgent = true;  // its camera ray is made in the next iteration's phase
-      }
+      else
+        need_jit = true;  // next sample of the block, same stream
     }
     PROF_MARK(PF_END);
     SEC(SC_LATCH);

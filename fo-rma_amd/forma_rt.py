@@ -89,7 +89,7 @@ EXPORTS = (
     "fr_ctx_wait", "fr_ctx_device_buffers", "fr_host_alloc", "fr_host_free", "fr_ctx_trace_log",
     "fr_ctx_trace_log_read", "fr_mctx_create", "fr_mctx_free", "fr_mctx_count", "fr_mctx_ctx", "fr_mctx_render",
     "fr_mctx_sync", "fr_mctx_frame", "fr_mctx_download",
-    "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_rng_camera", "fr_selftest_recip",
+    "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_recip",
     "fr_post_process", "fr_post_process_device", "fr_rgb_to_rgba_device", "fr_ctx_jit_info", "fr_selftest_jit",
     "fr_ctx_prepare", "fr_ctx_jit_state", "fr_jit_wait",
 )
@@ -168,8 +168,6 @@ def lib():
     L.fr_render_hip_multi.argtypes = [vp, P(FrCamera), P(FrParams), C.c_int, f3, P(C.c_uint8), P(FrStats)]
     L.fr_selftest_ops.argtypes = [C.c_int, C.c_int, f3, f3, C.c_uint32, f3]
     L.fr_selftest_rng.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
-    if hasattr(L, "fr_selftest_rng_camera"):  # (A/B builds of earlier revisions lack it)
-        L.fr_selftest_rng_camera.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32)]
     if hasattr(L, "fr_post_process"):  # absent from A/B builds of older sources
         L.fr_post_process.argtypes = [C.c_int, P(C.c_int), C.c_uint32, C.c_float, C.c_uint32, C.c_uint32,
                                       P(C.c_uint8), P(C.c_uint8)]

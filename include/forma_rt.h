@@ -313,10 +313,7 @@ int fr_rgb_to_rgba_device(void* stream, const uint8_t* d_rgb, uint8_t* d_rgba, s
 /* Run the device f32/RNG primitives on n inputs (op codes in DESIGN.md §7); used by the
    parity tests to show the GPU arithmetic is bit-identical to the host's. */
 int fr_selftest_ops(int device, int op, const float* a, const float* b, uint32_t n, float* out);
-/* The first n words of the scatter stream (fr_selftest_rng) and of the camera stream
-   (fr_selftest_rng_camera) of (seed, pixel, stream key = sample) as the kernel seeds them. */
 int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out);
-int fr_selftest_rng_camera(int device, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out);
 /* Compare the device's fast reciprocal (rcp + one Newton step) with the correctly rounded
    1.0f / x for every f32 bit pattern in [base, base + count): mismatches per exponent
    field in bad[256], first mismatching pattern in first[256] (0xFFFFFFFF = none). */

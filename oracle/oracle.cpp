@@ -74,11 +74,9 @@ struct ReflectRecord {
 };
 
 // ---- the RNG that replaces rand::thread_rng() -------------------------------
-// splitmix64 (Steele, Lea & Flood 2014) on x = seed ^ (pixel << 32 | stream key) keys two
-// xoshiro128+ 1.0 states (Blackman & Vigna 2018): outputs 1-2 the scatter stream, outputs
-// 3-4 the camera stream. A pixel's samples draw from their streams in order (stream_start
-// below): the jitter and lens draws of each sample from the camera stream, its scatter
-// draws from the scatter stream (the reference's save_image draws every sample from one
+// splitmix64 (Steele, Lea & Flood 2014) keys xoshiro128+ 1.0 (Blackman & Vigna
+// 2018) per (seed, pixel, stream key); a pixel's samples draw from their streams in
+// order (stream_start below; the reference's save_image draws every sample from one
 // sequential ThreadRng, tracer.rs:164-175); f32 = ((u32 ^ 2^31) >> 8) * 2^-24.
 struct Rng {
   uint32_t s[4];
@@ -89,13 +87,8 @@ struct Rng {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
   }
-  // camera = false: the scatter stream (splitmix outputs 1-2); true: the camera stream (3-4)
-  Rng(uint64_t seed, uint32_t pixel, uint32_t sample, bool camera = false) {
+  Rng(uint64_t seed, uint32_t pixel, uint32_t sample) {
     uint64_t x = seed ^ ((uint64_t(pixel) << 32) | uint64_t(sample));
-    if (camera) {
-      splitmix(x);
-      splitmix(x);
-    }
     uint64_t a = splitmix(x), b = splitmix(x);
     s[0] = uint32_t(a);
     s[1] = uint32_t(a >> 32);
@@ -676,14 +669,8 @@ void oracle_camera_translate(or_camera* cam, const float delta[3]) {
   c.to_c(cam);
 }
 
-// the first n words of the scatter stream of (seed, pixel, key), and of its camera stream
 void oracle_rng_stream(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
   Rng r(seed, pixel, sample);
-  for (uint32_t i = 0; i < n; ++i) out[i] = r.next_u32();
-}
-
-void oracle_rng_stream_camera(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
-  Rng r(seed, pixel, sample, true);
   for (uint32_t i = 0; i < n; ++i) out[i] = r.next_u32();
 }
 
@@ -801,18 +788,14 @@ int64_t oracle_render_rows(const or_prim* prims, uint32_t n, const or_camera* ca
         const uint32_t x = c * col_step;
         const uint32_t pixel = y * width + x;
         Vec3 col = Vec3::zero();
-        Rng rng(seed, pixel, 0), crng(seed, pixel, 0, true);
+        Rng rng(seed, pixel, 0);
         for (uint32_t s = 0; s < spp; ++s) {
-          // samples come in streams of 16 (4 in the last block); each draws in order, its
-          // camera draws from the camera stream and its scatter draws from the scatter stream
+          // samples come in streams of 16 (4 in the last block); each draws in order
           uint32_t key;
-          if (stream_start(s, spp, key)) {
-            rng = Rng(seed, pixel, key);
-            crng = Rng(seed, pixel, key, true);
-          }
-          const float u = (float(x) + crng.gen_f32()) / float(width);
-          const float v = (float(height - y) + crng.gen_f32()) / float(height);
-          const Ray ray = camera.get_ray(u, v, crng);
+          if (stream_start(s, spp, key)) rng = Rng(seed, pixel, key);
+          const float u = (float(x) + rng.gen_f32()) / float(width);
+          const float v = (float(height - y) + rng.gen_f32()) / float(height);
+          const Ray ray = camera.get_ray(u, v, rng);
           col = col + get_color(ray, objects, 0, max_depth, rng, cnt);
         }
         col = col / float(spp);
@@ -868,7 +851,6 @@ int oracle_render_mt(const or_prim* prims, uint32_t n, const or_camera* cam, uin
   const float t_offset = 1.0f / float(NTHREADS);
   std::vector<float> acc(size_t(width) * height * 3, 0.0f);
   std::vector<Rng> streams(size_t(width) * height, Rng(seed, 0, 0));
-  std::vector<Rng> cstreams(size_t(width) * height, Rng(seed, 0, 0, true));
   Counters cnt;
   for (uint32_t pass = 0; pass < sample; ++pass) {
     std::vector<uint8_t> pixels(size_t(width) * height * 3, 0);  // render_mt's result, bands stacked
@@ -878,16 +860,12 @@ int oracle_render_mt(const or_prim* prims, uint32_t n, const or_camera* cam, uin
           const uint32_t row = (NTHREADS - 1 - t_id) * t_height + y;  // ids sorted descending (:122-127)
           const uint32_t pixel = row * width + x;
           Rng& rng = streams[pixel];
-          Rng& crng = cstreams[pixel];
           uint32_t key;
-          if (stream_start(pass, sample, key)) {
-            rng = Rng(seed, pixel, key);
-            crng = Rng(seed, pixel, key, true);
-          }
-          const float u = (float(x) + crng.gen_f32()) / float(width);
-          float v = (float(t_height - y) + crng.gen_f32()) / float(height);
+          if (stream_start(pass, sample, key)) rng = Rng(seed, pixel, key);
+          const float u = (float(x) + rng.gen_f32()) / float(width);
+          float v = (float(t_height - y) + rng.gen_f32()) / float(height);
           v += float(t_id) * t_offset;
-          const Ray ray = camera.get_ray(u, v, crng);
+          const Ray ray = camera.get_ray(u, v, rng);
           const Vec3 color = get_color(ray, objects, 0, max_depth, rng, cnt);
           const size_t index = size_t(pixel) * 3;
           pixels[index] = as_u8(sqrtf(color.r()) * 255.0f);

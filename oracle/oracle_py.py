@@ -44,7 +44,6 @@ def lib():
         L.oracle_camera_orbit.argtypes = [C.POINTER(OrCamera), f3]
         L.oracle_camera_translate.argtypes = [C.POINTER(OrCamera), f3]
         L.oracle_rng_stream.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
-        L.oracle_rng_stream_camera.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
         L.oracle_vec3.argtypes = [C.c_int, f3, f3, f3]
         L.oracle_refract.argtypes = [f3, f3, C.c_float, f3]
         L.oracle_refract.restype = C.c_int
@@ -110,10 +109,9 @@ def camera_to_array(cam):
     return np.asarray(vals, dtype=np.float32)
 
 
-def rng_stream(seed, pixel, sample, n, camera=False):
-    """the first n words of the scatter (or camera) stream of (seed, pixel, stream key)"""
+def rng_stream(seed, pixel, sample, n):
     out = (C.c_uint32 * n)()
-    (lib().oracle_rng_stream_camera if camera else lib().oracle_rng_stream)(seed, pixel, sample, n, out)
+    lib().oracle_rng_stream(seed, pixel, sample, n, out)
     return np.frombuffer(out, dtype=np.uint32).copy()
 
 

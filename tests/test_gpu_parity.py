@@ -266,8 +266,6 @@ def test_device_rng_matches_oracle(gpu, seed, pixel, sample):
     out = (C.c_uint32 * 200)()
     gpu.check(gpu.lib().fr_selftest_rng(0, seed, pixel, sample, 200, out))
     assert list(out) == list(O.rng_stream(seed, pixel, sample, 200))
-    gpu.check(gpu.lib().fr_selftest_rng_camera(0, seed, pixel, sample, 200, out))
-    assert list(out) == list(O.rng_stream(seed, pixel, sample, 200, camera=True))
 
 
 # ---- images -----------------------------------------------------------------------

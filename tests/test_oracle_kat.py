@@ -233,9 +233,3 @@ def test_oracle_rng_matches_restatement(seed, pixel, sample):
     x, b = _splitmix(x)
     want = _xoshiro([a & 0xFFFFFFFF, a >> 32, b & 0xFFFFFFFF, b >> 32], 64)
     assert list(O.rng_stream(seed, pixel, sample, 64)) == want
-    # the camera stream: splitmix64 outputs 3 and 4 of the same x
-    x, c = _splitmix(x)
-    x, e = _splitmix(x)
-    want_c = _xoshiro([c & 0xFFFFFFFF, c >> 32, e & 0xFFFFFFFF, e >> 32], 64)
-    assert list(O.rng_stream(seed, pixel, sample, 64, camera=True)) == want_c
-    assert want_c != want

@@ -24,14 +24,14 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "fo-rma_amd", "csrc")
 # counted regions, in trace_kernel.h's SC_* order
-REGIONS = ["SC_ITER", "SC_CLAIM", "SC_SETUP", "SC_PHASE", "SC_FLUSH", "SC_JIT", "SC_LENS", "SC_CAM", "SC_TAKE", "SC_NEED",
-           "SC_REJ", "SC_SCAT", "SC_HIT", "SC_SKY", "SC_SHADE", "SC_END", "SC_FLUSH2", "SC_FLUSHC"]
+REGIONS = ["SC_ITER", "SC_CLAIM", "SC_JIT", "SC_NEED", "SC_REJ", "SC_CAM", "SC_SCAT", "SC_HIT", "SC_SKY", "SC_SHADE",
+           "SC_END"]
 # marker-only regions: the counted region whose entries they share
-DERIVED = {"SC_ACC": "SC_NEED", "SC_POSTHIT": "SC_HIT", "SC_POSTSHADE": "SC_ITER", "SC_LATCH": "SC_ITER"}
+DERIVED = {"SC_SETUP": "SC_CLAIM", "SC_ACC": "SC_NEED", "SC_POSTHIT": "SC_HIT", "SC_POSTSHADE": "SC_ITER",
+           "SC_LATCH": "SC_ITER"}
 # render.hip jit_defines() for the default build
 DEFINES = dict(FR_KREJ=4, FR_KREJ_NIB=9, FR_CLAIM_MIN=1, FR_CLAIM_MIN_NIB=3, FR_NUM_SGPR=96, FR_BLOCK_SAMPLES=16,
-               FR_FINE_SAMPLES=4, FR_STAGE=4, FR_BVH_STAGE=2, FR_NIB_WAVES=8, FR_DIFF12_WAVES=7, FR_CAMB=1, FR_CAM_MIN=40,
-               FR_KLENS=4)
+               FR_FINE_SAMPLES=4, FR_STAGE=4, FR_BVH_STAGE=2, FR_NIB_WAVES=8, FR_DIFF12_WAVES=7)
 OPTS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt",
         "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize"]
 
