@@ -258,8 +258,10 @@ __host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? FR
 #ifndef FR_BVH_RSTAGE
 #define FR_BVH_RSTAGE 0
 #endif
-// a sub-block starts on a staging group: the group's store covers only its own samples
-static_assert(kFineSamples % FR_STAGE == 0, "sub-blocks hold whole staging groups");
+// A staging group larger than a sub-block (FR_STAGE 8): a sub-block's group store starts at
+// the sub-block's first sample, so it never writes another sub-block's slots.
+static_assert(kFineSamples % FR_STAGE == 0 || FR_STAGE % kFineSamples == 0, "staging groups and sub-blocks nest");
+constexpr bool kStageSpansSub = FR_STAGE > kFineSamples;
 
 // FR_DIAG builds count, per phase, wave-level trips (one per SIMT pass of the wave)
 // and lane-level work, to measure SIMT efficiency. Never enabled in the product.
@@ -307,8 +309,8 @@ enum { PF_CLAIM, PF_REJ, PF_HIT, PF_SHADE, PF_END, PF_N };
 // The first SC_N regions are counted; the others only mark a boundary in the listing, and
 // their entries follow from a counted one (SETUP ~ CLAIM, ACC = NEED, POSTHIT = HIT,
 // POSTSHADE = LATCH = ITER; GRAB = the batches the queue hands out).
-enum { SC_ITER, SC_CLAIM, SC_JIT, SC_NEED, SC_REJ, SC_CAM, SC_SCAT, SC_HIT, SC_SKY, SC_SHADE, SC_END, SC_N,
-       SC_GRAB = SC_N, SC_SETUP, SC_ACC, SC_POSTHIT, SC_POSTSHADE, SC_LATCH };
+enum { SC_ITER, SC_CLAIM, SC_JIT, SC_NEED, SC_REJ, SC_CAM, SC_SCAT, SC_HIT, SC_SKY, SC_SHADE, SC_END, SC_NODE,
+       SC_LEAF, SC_LTEST, SC_N, SC_GRAB = SC_N, SC_SETUP, SC_ACC, SC_POSTHIT, SC_POSTSHADE, SC_LATCH };
 #if defined(FR_SEC_MARKS) && defined(__HIP_DEVICE_COMPILE__)
 #define SEC(k) asm volatile(";FRSEC " #k)
 #elif defined(FR_SECCNT)
@@ -558,7 +560,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   float sfuzz = 0.0f, fx = 0.0f, fy = 0.0f, vofs = 0.0f;
   bool smetal = false;
   uint32_t sbest = 0, s = 0, s_end = 0, nseg = 0, nhit = 0;  // (scatters = segments - samples: the host's)
-  uint32_t jj = 0;           // sample index within the item's block
+  // (a sample's index within its block is s mod kBlockSamples: blocks start at multiples of it)
+  static_assert((kBlockSamples & (kBlockSamples - 1u)) == 0u, "blocks of a power-of-two sample count");
+  uint32_t jfirst = 0;       // kStageSpansSub: the item's first sample in the block
   V3 pend{0.0f, 0.0f, 0.0f};  // RSTG: the pair's first colour (an even jj)
 #ifdef FR_DIAG
   uint32_t diag_tb = 0, diag_seg0 = 0;  // the item's batch index, segments at its claim
@@ -714,8 +718,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           // (item - k * P in the buffer); a whole block: k = 0
           const uint32_t k = (b >> 28) & 3u;
           const bool fine = (b & kFineKey) != 0u;
-          jj = k * kFineSamples;
-          s = (b & 0x0FFFFFFFu) * kBlockSamples + jj;
+          const uint32_t j0 = k * kFineSamples;
+          if (kStageSpansSub) jfirst = j0;
+          s = (b & 0x0FFFFFFFu) * kBlockSamples + j0;
           out = kw.samples + WPS * (static_cast<size_t>(item - k * kp.P) * kp.ks);
 #ifdef FR_DIAG
           diag_tb = item >> 6;
@@ -885,6 +890,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           const V3 oinv{o.x * invc.x, o.y * invc.y, o.z * invc.z};
           while (ref != kBvhEnd) {
             while (ref < kBvhLeaf) {
+              SEC(SC_NODE);
               DIAG_WAVE(DG_NODE_W);
               DIAG_LANE(DG_NODE_L);
               // internal node: both children's boxes
@@ -922,12 +928,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               }
             }
             if (ref == kBvhEnd) break;
+            SEC(SC_LEAF);
             DIAG_WAVE(DG_LEAF_W);
             DIAG_LANE(DG_LEAF_L);
             // leaf: slots [first, first + count) of the leaf-order records
             const uint32_t first = ref & ((1u << kBvhSlotBits) - 1u);
             const uint32_t cnt = ((ref >> kBvhSlotBits) & 15u) + 1u;
             for (uint32_t kk = 0; kk < cnt; ++kk) {
+              SEC(SC_LTEST);
               const uint32_t slot = first + kk;
               const uint32_t i = sc.bvh_order[slot];
               const float4* r = sc.lrec + 4 * slot;
@@ -1233,6 +1241,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           for (int j = udepth - 1; j >= 0; --j) col = mul(xyz(sc.att[stack[j * kBlock + tid]]), col);
         }
       }
+      const uint32_t jj = s & (kBlockSamples - 1u);  // the sample's index in its block
       if (RSTG) {
         // pairs start on even jj (blocks and sub-blocks do): the odd sample stores both
         if (jj & 1u) {
@@ -1274,13 +1283,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         if (WPS == 3) sl[2] = col.z;
         const bool full = (jj & (STG - 1u)) == STG - 1u;
         if (full || s + 1u == s_end) {
-          float* dst = out + WPS * (jj & ~(STG - 1u));
-          if (full && kp.ks == kBlockSamples) {
+          const uint32_t g0 = jj & ~(STG - 1u);
+          // (a sub-block inside a wider group stores from its own first sample)
+          const uint32_t lo = kStageSpansSub ? max(g0, jfirst) : g0;
+          float* dst = out + WPS * g0;
+          if (full && kp.ks == kBlockSamples && lo == g0) {
             if constexpr ((WPS * STG) % 4u == 0u) {
               // 16-B aligned: item * 192 (128) B + a multiple of 48 (32) B
               const float4* src = reinterpret_cast<const float4*>(stage);
 #pragma unroll
-              for (uint32_t k = 0; k < WPS * STG / 4u; ++k) reinterpret_cast<float4*>(dst)[k] = src[k];
+              for (uint32_t k = 0; k < WPS * STG / 4u; ++k) {
+                reinterpret_cast<float4*>(dst)[k] = src[k];
+#if defined(__HIP_DEVICE_COMPILE__)
+                // wide groups: two 16-B stores at a time, not every LDS read first (registers)
+                if (WPS * STG > 8u) asm volatile("" ::: "memory");
+#endif
+              }
             } else {
               // 8-B aligned: item * 192 B + a multiple of 24 B
               const float2* src = reinterpret_cast<const float2*>(stage);
@@ -1288,11 +1306,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               for (uint32_t k = 0; k < WPS * STG / 2u; ++k) reinterpret_cast<float2*>(dst)[k] = src[k];
             }
           } else {
-            for (uint32_t k = 0; k < WPS * ((jj & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
+            for (uint32_t k = WPS * (lo - g0); k < WPS * ((jj & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
           }
         }
       }
-      ++jj;
 #ifdef FR_DIAG
       if (s + 1u == s_end && diag_tb < (1u << 20)) atomicAdd(&g_fr_tb_cost[diag_tb], nseg - diag_seg0);
 #endif

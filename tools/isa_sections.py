@@ -9,7 +9,8 @@ are counted (v_* opcodes; SALU, LDS and memory instructions separately).
 Dynamic side: an FR_SECCNT build of the library counts how many times a wave enters each
 region per launch (the FR_SECCNT line on stderr, captured on the GPU box).
 
-    python tools/isa_sections.py isa  [--template 1,0,9,8,0,0,2,1]   -> static table (JSON)
+    python tools/isa_sections.py isa [--template=1,0,9,8,0,0,2,1] [--nojit] [-DNAME=V]  -> static table (JSON)
+      (--nojit: the compiled-in kernel, e.g. --template=2,0,4,8,1,0,0,1 --nojit for C5's BVH kernel)
     python tools/isa_sections.py combine STATIC.json SECCNT_LINE_FILE SEGMENTS VALU_MEASURED [GRABS]
 
 combine multiplies the two: VALU instructions per region per launch, their share, and the
@@ -25,7 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "fo-rma_amd", "csrc")
 # counted regions, in trace_kernel.h's SC_* order
 REGIONS = ["SC_ITER", "SC_CLAIM", "SC_JIT", "SC_NEED", "SC_REJ", "SC_CAM", "SC_SCAT", "SC_HIT", "SC_SKY", "SC_SHADE",
-           "SC_END"]
+           "SC_END", "SC_NODE", "SC_LEAF", "SC_LTEST"]
 # marker-only regions: the counted region whose entries they share
 DERIVED = {"SC_SETUP": "SC_CLAIM", "SC_ACC": "SC_NEED", "SC_POSTHIT": "SC_HIT", "SC_POSTSHADE": "SC_ITER",
            "SC_LATCH": "SC_ITER"}
@@ -49,20 +50,21 @@ def scene08_records():
     return words
 
 
-def build_isa(targs, extra_defs=()):
+def build_isa(targs, extra_defs=(), jit=True):
     out = os.path.join(ROOT, "fo-rma_amd", "build", "isa_jit")
     os.makedirs(out, exist_ok=True)
-    recs = scene08_records()
     pre = "".join(f"#define {k} {v}\n" for k, v in DEFINES.items())
-    pre += f"#define FR_JIT_N {len(recs)}u\n#define FR_JIT_REC " + ",".join(
-        "{" + ",".join(f"0x{w:08x}u" for w in r) + "}" for r in recs) + "\n"
+    if jit:  # the scene-specialised build (scene_08's records); else the compiled-in kernel
+        recs = scene08_records()
+        pre += f"#define FR_JIT_N {len(recs)}u\n#define FR_JIT_REC " + ",".join(
+            "{" + ",".join(f"0x{w:08x}u" for w in r) + "}" for r in recs) + "\n"
     ta = targs
     inst = (f"template __global__ void fr::trace_kernel<{ta[0]}, {'true' if ta[1] else 'false'}, {ta[2]}, {ta[3]}, "
             f"{'true' if ta[4] else 'false'}, {'true' if ta[5] else 'false'}, {ta[6]}, {ta[7]}>(fr::KArgs);\n")
-    src = os.path.join(out, "scene08_kernel.hip")
+    src = os.path.join(out, "scene08_kernel.hip" if jit else "kernel_%s.hip" % "_".join(map(str, targs)))
     with open(src, "w") as f:
         f.write(pre + '#include "trace_kernel.h"\n' + inst)
-    asm = os.path.join(out, "scene08_kernel.s")
+    asm = src[:-4] + ".s"
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-I", CSRC, "-I",
            os.path.join(ROOT, "include"), *OPTS, "-DFR_SEC_MARKS", *extra_defs, src, "-o", asm]
     subprocess.run(cmd, check=True)
@@ -173,12 +175,15 @@ if __name__ == "__main__":
     if sys.argv[1] == "isa":
         targs = [1, 0, 9, 8, 0, 0, 2, 1]
         extra = []
+        jit = True
         for a in sys.argv[2:]:
             if a.startswith("--template="):
                 targs = [int(x) for x in a.split("=", 1)[1].split(",")]
+            elif a == "--nojit":
+                jit = False
             elif a.startswith("-D"):
                 extra.append(a)
-        asm = build_isa(targs, extra)
+        asm = build_isa(targs, extra, jit)
         tab, meta = count_regions(asm)
         print(json.dumps({"template": targs, "asm": os.path.relpath(asm, ROOT), "meta": meta, "regions": tab},
                          indent=1))
