@@ -83,6 +83,9 @@ struct DeviceCopy {
   bool bvh_ok = false;  // segments and trees built (else the in-order loop only)
   float bvh_extent = 0; // largest |coordinate| of the primitives' bounds (bvh.h)
   uint32_t n_segs = 0;  // closest-hit segments: BVH runs and planes (bvh.h)
+  // traversal-stack levels a lane can use: the trees' largest internal-node depth + 1 (a
+  // lane at depth d holds at most d entries and writes the free one): the BVH launch's LDS
+  uint32_t bvh_levels = kBvhStack;
   bool att_nonneg = true;  // every attenuation component finite and >= +0 (no -0)
   bool diffuse = true;     // no metal or dielectric scatter class (trace_kernel MAT = 1)
   std::vector<uint32_t> rec_words;  // the n 64-B records as uploaded (the scene-specialised build's constants)
@@ -281,6 +284,7 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   c->bvh_ok = bvh_ok;
   c->bvh_extent = bvh_extent;
   c->n_segs = static_cast<uint32_t>(bvh_segs.size());
+  c->bvh_levels = bvh_ok ? std::min(bvh_max_depth(bvh_segs, bvh_nodes) + 1u, kBvhStack) : kBvhStack;
   for (uint32_t i = 0; i < n; ++i) {
     const fr_prim& p = s->prims[i];
     uint32_t kind = p.kind;
@@ -571,10 +575,13 @@ static int launch_persistent(const Grid& g, size_t lds, hipStream_t st, KArgs a,
   if (oe != hipSuccess || per_cu < 1) per_cu = 1;
   // the per-wave counter slots (fr_ctx::d_wcnt) hold kMaxWgPerCu workgroups per CU
   if (per_cu > static_cast<int>(kMaxWgPerCu)) per_cu = static_cast<int>(kMaxWgPerCu);
-  // FR_BVH_STAGE: "0" BVH kernels store unstaged, "1" staged even at a lower residency (A/B, tests)
+  // BVH kernels store their samples unstaged unless FR_BVH_STAGE asks: "1" staged even at a
+  // lower residency, "2" staged when it costs no residency (A/B, tests). At 7 workgroups per
+  // CU the pair staging measured slower than plain stores (C5 51.45 ms unstaged, 51.87
+  // staged; with 8-bin trees 48.39 / 48.63); at 6 it had paid (66.8 -> 64.3 ms, round 2).
   const char* stage_env = getenv("FR_BVH_STAGE");
   const bool force_stage = stage_env && strcmp(stage_env, "1") == 0;
-  if (g.stage_bytes && !(stage_env && strcmp(stage_env, "0") == 0)) {
+  if (g.stage_bytes && stage_env && (force_stage || strcmp(stage_env, "2") == 0)) {
     int staged = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&staged, kern, static_cast<int>(kBlock), lds + g.stage_bytes) ==
             hipSuccess &&
@@ -969,7 +976,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
   const size_t stage_n = stage_samples(use_bvh);
   const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * wps * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
-                     n_rec * 64 + stack_bytes + (use_bvh ? kBvhStack * kBlock * sizeof(uint32_t) : 0u);
+                     n_rec * 64 + stack_bytes + (use_bvh ? dc->bvh_levels * kBlock * sizeof(uint32_t) : 0u);
   // the scene-specialised kernel (jit.h): list-loop scenes of <= kJitMaxPrims primitives,
   // when the caller asks (FR_FLAG_SCENE_JIT; FR_SCENE_JIT=1 / 0 forces it on / off)
   JitReq jr;
@@ -1184,11 +1191,12 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
             "FR_DIAG {\"iter_w\": %llu, \"regen_w\": %llu, \"regen_l\": %llu, \"hit_w\": %llu, \"end_w\": %llu, "
             "\"end_l\": %llu, \"unwind_w\": %llu, \"unwind_l\": %llu, \"lens_w\": %llu, \"lens_l\": %llu, "
             "\"rus_w\": %llu, \"rus_l\": %llu, \"merged_w\": %llu, \"merged_l\": %llu, \"segments\": %llu, "
-            "\"hits\": %llu, \"node_w\": %llu, \"node_l\": %llu, \"leaf_w\": %llu, \"leaf_l\": %llu}\n",
+            "\"hits\": %llu, \"node_w\": %llu, \"node_l\": %llu, \"leaf_w\": %llu, \"leaf_l\": %llu, "
+            "\"node_coh_w\": %llu, \"node_u2_w\": %llu, \"node_u34_w\": %llu, \"node_primary_l\": %llu}\n",
             cnt[4 + DG_ITER], cnt[4 + DG_REGEN_W], cnt[4 + DG_REGEN_L], cnt[4 + DG_HIT_W], cnt[4 + DG_END_W],
             cnt[4 + DG_END_L], cnt[4 + DG_UNW_W], cnt[4 + DG_UNW_L], dl[0], dl[1], dr[0], dr[1], cnt[4 + DG_LENS_W],
             cnt[4 + DG_LENS_L], cnt[0], cnt[1], cnt[4 + DG_NODE_W], cnt[4 + DG_NODE_L], cnt[4 + DG_LEAF_W],
-            cnt[4 + DG_LEAF_L]);
+            cnt[4 + DG_LEAF_L], cnt[4 + DG_NCOH_W], cnt[4 + DG_NU2_W], cnt[4 + DG_NU4_W], cnt[4 + DG_NPRIM_L]);
     if (const char* path = getenv("FR_DIAG_COST")) {
       std::vector<unsigned int> tc(1u << 20);
       HIPCHK(hipMemcpyFromSymbol(tc.data(), HIP_SYMBOL(g_fr_tb_cost), tc.size() * 4));

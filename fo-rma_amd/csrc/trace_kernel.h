@@ -253,6 +253,16 @@ constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for smal
 #define FR_BVH_STAGE 2
 #endif
 __host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? FR_BVH_STAGE : FR_STAGE; }
+// FR_BVH_SCALAR_NODES=1: a node step whose walking lanes are all at one node reads it with
+// scalar loads (0, vector loads only: C5 trace 52.9 -> 62.3 ms, the vector memory path
+// returning 64 B per lane per step)
+#ifndef FR_BVH_SCALAR_NODES
+#define FR_BVH_SCALAR_NODES 1
+#endif
+// FR_BVH_SCALAR_LEAVES=1: a leaf every lane is at is tested from scalar loads (A/B knob)
+#ifndef FR_BVH_SCALAR_LEAVES
+#define FR_BVH_SCALAR_LEAVES 1
+#endif
 // FR_BVH_RSTAGE=1: the BVH kernels hold a pair's first colour in registers instead of LDS
 // (3 VGPRs, none of the traversal stack's LDS), so every BVH launch stores whole pairs.
 #ifndef FR_BVH_RSTAGE
@@ -267,7 +277,8 @@ constexpr bool kStageSpansSub = FR_STAGE > kFineSamples;
 // and lane-level work, to measure SIMT efficiency. Never enabled in the product.
 #ifdef FR_DIAG
 enum { DG_ITER, DG_REGEN_W, DG_REGEN_L, DG_LENS_W, DG_LENS_L, DG_RUS_W, DG_RUS_L, DG_END_W, DG_END_L,
-       DG_UNW_W, DG_UNW_L, DG_HIT_W, DG_NODE_W, DG_NODE_L, DG_LEAF_W, DG_LEAF_L, DG_N };
+       DG_UNW_W, DG_UNW_L, DG_HIT_W, DG_NODE_W, DG_NODE_L, DG_LEAF_W, DG_LEAF_L, DG_NCOH_W, DG_NU2_W, DG_NU4_W,
+       DG_NPRIM_L, DG_N };
 #define DIAG_WAVE(slot)                                                         \
   do {                                                                          \
     const unsigned long long m_ = __ballot(1);                                  \
@@ -332,6 +343,29 @@ __device__ __forceinline__ uint32_t lanes_set(bool b) {
   const unsigned long long m = __builtin_amdgcn_ballot_w64(b);
   return static_cast<uint32_t>(__builtin_popcount(static_cast<uint32_t>(m)) +
                                __builtin_popcount(static_cast<uint32_t>(m >> 32)));
+}
+
+// Per-lane select on a lane mask (a ballot): one v_cndmask_b32. The compiler turned chains
+// of selects on compare results into branches with the conditions materialised as 0/1
+// values in VGPRs; masks combined with SALU ops and this select keep them in SGPRs.
+// Lanes whose v < s (unsigned), as a lane mask.
+__device__ __forceinline__ unsigned long long lanes_lt_u32(uint32_t v, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned long long m;
+  asm("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(m) : "s"(s), "v"(v));
+  return m;
+#else
+  return v < s;  // device only
+#endif
+}
+__device__ __forceinline__ uint32_t lane_sel(unsigned long long m, uint32_t if_set, uint32_t if_clear) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+  return r;
+#else
+  return if_set;  // device only
+#endif
 }
 
 // Pixel slot q of a shard -> image coordinates. Slots run tile by tile (8x8 pixels,
@@ -446,8 +480,14 @@ template <int KS, bool HAS_PLANE, int KREJ, int MAXD, bool BVH, bool MT, int DEF
 #ifndef FR_DIFF12_WAVES
 #define FR_DIFF12_WAVES 7  // diffuse-only 12-B-record kernels (A/B knob)
 #endif
-#define FR_OCC_ATTR \
-  __attribute__((amdgpu_waves_per_eu(BVH ? 6 : DEFER == 2 ? FR_NIB_WAVES : (DEFER == 1 && MAT == 1) ? FR_DIFF12_WAVES : 7)))
+#ifndef FR_BVH_WAVES
+// BVH kernels: 7 (72 VGPRs, one value spilled to scratch in the scatter step) over 6 (74
+// VGPRs with the split scalar/vector node step): C5 trace 54.0 -> 51.4 ms
+#define FR_BVH_WAVES 7
+#endif
+#define FR_OCC_ATTR                                                                                      \
+  __attribute__((amdgpu_waves_per_eu(BVH ? FR_BVH_WAVES : DEFER == 2 ? FR_NIB_WAVES                   \
+                                                      : (DEFER == 1 && MAT == 1) ? FR_DIFF12_WAVES : 7)))
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR))) FR_OCC_ATTR void trace_kernel(
     KArgs args) {
@@ -875,7 +915,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
             continue;
           }
           uint32_t ref = sp[1];
-          uint32_t depth_s = 0;  // entries on this lane's traversal stack
+          // this lane's next free traversal-stack entry, an index into tstack (level-major:
+          // one level is kBlock entries); the stack is empty while it is in level 0
+          uint32_t tso = tid;
           // node slabs as fma(lo, inv, -o inv): a cull only, covered by the padding for
           // origins within kBvhOriginReach scene extents (bvh.h; the host checks the camera).
           // The cull's reciprocal is clamped to +-2^100 (bvh.h kBvhInvClamp): an exact-zero
@@ -893,52 +935,78 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               SEC(SC_NODE);
               DIAG_WAVE(DG_NODE_W);
               DIAG_LANE(DG_NODE_L);
-              // internal node: both children's boxes
-              float4 na, nb, nc;
-              uint4 nr;
+#ifdef FR_DIAG
+              {
+                // distinct nodes among the walking lanes (1, 2, 3-4, more), and lanes of primary rays
+                unsigned long long m_ = __ballot(1);
+                uint32_t u_ = 0;
+                while (m_ && u_ < 5) {
+                  const uint32_t r_ = __builtin_amdgcn_readlane(ref, __ffsll(m_) - 1);
+                  m_ &= ~__ballot(ref == r_);
+                  ++u_;
+                }
+                if (u_ == 1) DIAG_WAVE(DG_NCOH_W);
+                if (u_ == 2) DIAG_WAVE(DG_NU2_W);
+                if (u_ == 3 || u_ == 4) DIAG_WAVE(DG_NU4_W);
+                if (depth == 0) DIAG_LANE(DG_NPRIM_L);
+              }
+#endif
+              // the stack's top, read before the node arrives (level 0's own entry, unused,
+              // when the stack is empty)
+              typedef unsigned long long Mask;  // lane masks (ballots of single compares)
+              // (the compare in asm: the compiler fused it with tso - kBlock into a borrow,
+              // materialised as 0/1 and compared again for the ballot)
+              const uint32_t tdown = tso - kBlock;
+              const Mask mempty = lanes_lt_u32(tso, kBlock);
+              const uint32_t top = tstack[lane_sel(mempty, tso, tdown)];
+              // internal node: both children's boxes; the nearer entered child next (the
+              // left one on a tie) and the other stacked when both are entered; neither: the
+              // stack's top. Branch-free: the far child is written to the free entry either
+              // way (a node at depth d has at most d entries below it, d < kBvhStack) and the
+              // index moves only on a push or pop. (A ballot of an & of compares went through
+              // a 0/1 VGPR and a compare: the compares' own masks are combined with SALU ops.)
+              auto node_step = [&](const float4 na, const float4 nb, const float4 nc, const uint32_t cl,
+                                   const uint32_t cr) {
+                const Slab sl = slab3_fused(xyz(na), xyz(nb), oinv, invc);
+                const Slab sr = slab3_fused(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, oinv, invc);
+                const Mask ml = __builtin_amdgcn_ballot_w64(sl.tn <= sl.tf) &
+                                __builtin_amdgcn_ballot_w64(sl.tf >= 0.001f) & __builtin_amdgcn_ballot_w64(sl.tn <= closest);
+                const Mask mr = __builtin_amdgcn_ballot_w64(sr.tn <= sr.tf) &
+                                __builtin_amdgcn_ballot_w64(sr.tf >= 0.001f) & __builtin_amdgcn_ballot_w64(sr.tn <= closest);
+                const Mask mgol = ml & (__builtin_amdgcn_ballot_w64(sl.tn <= sr.tn) | ~mr);
+                const Mask many = ml | mr;
+                tstack[tso] = lane_sel(mgol, cr, cl);
+                const uint32_t tpop = lane_sel(many | mempty, tso, tdown);
+                ref = lane_sel(many, lane_sel(mgol, cl, cr), lane_sel(mempty, kBvhEnd, top));
+                tso = lane_sel(ml & mr, tso + kBlock, tpop);
+              };
+#if FR_BVH_SCALAR_NODES
               const uint32_t ref0 = __builtin_amdgcn_readfirstlane(ref);
               if (__ballot(ref != ref0) == 0) {
-                // every walking lane is at the same node (coherent rays near the root):
-                // scalar loads, which return sooner than the vector path
+                // every walking lane is at the same node (a quarter of C5's node steps, primary
+                // rays of one tile): scalar loads, the slab arithmetic on SGPR operands (the
+                // distinct asm ends keep the two paths from being merged over copies of the
+                // node into VGPRs)
                 const RecRef nd = rec_at(sc.bvh, ref0);
-                na = nd[0];
-                nb = nd[1];
-                nc = nd[2];
                 const float4 r = nd[3];
-                nr = make_uint4(__float_as_uint(r.x), __float_as_uint(r.y), __float_as_uint(r.z), __float_as_uint(r.w));
-              } else {
-                na = sc.bvh[4 * ref];
-                nb = sc.bvh[4 * ref + 1];
-                nc = sc.bvh[4 * ref + 2];
-                nr = reinterpret_cast<const uint4*>(sc.bvh)[4 * ref + 3];
-              }
-              const Slab sl = slab3_fused(xyz(na), xyz(nb), oinv, invc);
-              const Slab sr = slab3_fused(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, oinv, invc);
-              const bool hl = (sl.tn <= sl.tf) & (sl.tf >= 0.001f) & (sl.tn <= closest);
-              const bool hr = (sr.tn <= sr.tf) & (sr.tf >= 0.001f) & (sr.tn <= closest);
-              if (hl & hr) {
-                const bool lfirst = sl.tn <= sr.tn;
-                tstack[depth_s * kBlock + tid] = lfirst ? nr.y : nr.x;
-                ++depth_s;
-                ref = lfirst ? nr.x : nr.y;
-              } else if (hl | hr) {
-                ref = hl ? nr.x : nr.y;
-              } else {
-                ref = depth_s ? tstack[--depth_s * kBlock + tid] : kBvhEnd;
+                node_step(nd[0], nd[1], nd[2], __float_as_uint(r.x), __float_as_uint(r.y));
+                asm volatile("; bvh node step: scalar");
+              } else
+#endif
+              {
+                const uint32_t nb0 = ref * 64u;  // node byte offset (< 2^32: nodes < 2^26)
+                const uint4 nr = __builtin_bit_cast(uint4, buf_load4(sc.bvh, nb0 + 48u));
+                node_step(buf_load4(sc.bvh, nb0), buf_load4(sc.bvh, nb0 + 16u), buf_load4(sc.bvh, nb0 + 32u), nr.x, nr.y);
+                asm volatile("; bvh node step: vector");
               }
             }
             if (ref == kBvhEnd) break;
             SEC(SC_LEAF);
             DIAG_WAVE(DG_LEAF_W);
             DIAG_LANE(DG_LEAF_L);
-            // leaf: slots [first, first + count) of the leaf-order records
-            const uint32_t first = ref & ((1u << kBvhSlotBits) - 1u);
-            const uint32_t cnt = ((ref >> kBvhSlotBits) & 15u) + 1u;
-            for (uint32_t kk = 0; kk < cnt; ++kk) {
-              SEC(SC_LTEST);
-              const uint32_t slot = first + kk;
-              const uint32_t i = sc.bvh_order[slot];
-              const float4* r = sc.lrec + 4 * slot;
+            // leaf: slots [first, first + count) of the leaf-order records; one test of
+            // primitive i (list index) whose leaf-order record r is at `slot`
+            auto leaf_test = [&](const uint32_t i, const auto& r) {
               const float tmax =
                   static_cast<int>(i) < best ? __uint_as_float(__float_as_uint(closest) + 1u) : closest;
               const uint32_t k = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(r[3].w);
@@ -965,8 +1033,43 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                 best = static_cast<int>(i);
                 if (HAS_PLANE) t_last = t;
               }
+            };
+            const uint32_t first = ref & ((1u << kBvhSlotBits) - 1u);
+            const uint32_t cnt = ((ref >> kBvhSlotBits) & 15u) + 1u;
+#if FR_BVH_SCALAR_LEAVES
+            const uint32_t leaf0 = __builtin_amdgcn_readfirstlane(ref);
+            if (__ballot(ref != leaf0) == 0) {
+              // every lane at one leaf: its records through scalar loads
+              typedef __attribute__((address_space(4))) const uint32_t cu32l;
+              const cu32l* ord = (cu32l*)(reinterpret_cast<uintptr_t>(sc.bvh_order));
+              const uint32_t first0 = leaf0 & ((1u << kBvhSlotBits) - 1u);
+              const uint32_t cnt0 = ((leaf0 >> kBvhSlotBits) & 15u) + 1u;
+              for (uint32_t kk = 0; kk < cnt0; ++kk) {
+                SEC(SC_LTEST);
+                leaf_test(ord[first0 + kk], rec_at(sc.lrec, first0 + kk));
+              }
+              asm volatile("; bvh leaf: scalar");
+            } else
+#endif
+            {
+              for (uint32_t kk = 0; kk < cnt; ++kk) {
+                SEC(SC_LTEST);
+                const uint32_t slot = first + kk;
+                // buffer loads: 32-bit offsets from the arrays' bases (slots < 2^26)
+                struct LeafRec {
+                  const float4* base;
+                  uint32_t off;
+                  __device__ float4 operator[](uint32_t k) const { return buf_load4(base, off + 16u * k); }
+                } const r{sc.lrec, slot * 64u};
+                leaf_test(buf_load1(sc.bvh_order, slot * 4u), r);
+              }
+              asm volatile("; bvh leaf: vector");
             }
-            ref = depth_s ? tstack[--depth_s * kBlock + tid] : kBvhEnd;
+            {
+              const bool empty = tso < kBlock;
+              if (!empty) tso -= kBlock;
+              ref = empty ? kBvhEnd : tstack[tso];
+            }
           }
         }
       }

@@ -914,9 +914,9 @@ def test_record_formats_are_bit_identical(gpu, scene, spp, monkeypatch):
 
 @pytest.mark.parametrize("spp", [3, 21])
 def test_bvh_sample_staging_is_bit_identical(gpu, spp, monkeypatch):
-    """BVH kernels stage 2 samples per store when the LDS allows (KF_STAGE, the C5 scene);
-    FR_BVH_STAGE=0 stores each sample directly. Same bits, whole sub-blocks and partial
-    groups (spp 3, 21) included."""
+    """BVH kernels store each sample directly by default; FR_BVH_STAGE=2 stages 2 samples per
+    store when the LDS allows it (KF_STAGE, the C5 scene), 1 even at a lower residency. Same
+    bits, whole sub-blocks and partial groups (spp 3, 21) included."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("gen_scene", os.path.join(ROOT, "tools", "gen_scene.py"))
     gs = importlib.util.module_from_spec(spec)
@@ -926,10 +926,11 @@ def test_bvh_sample_staging_is_bit_identical(gpu, spp, monkeypatch):
     sc = gpu.Scene.from_json(text, w, h)
     monkeypatch.delenv("FR_BVH_STAGE", raising=False)
     ref = gpu.render(sc, sc.camera, w, h, spp, 8)
-    monkeypatch.setenv("FR_BVH_STAGE", "0")
-    mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, 8)
-    assert np.array_equal(mean.view(np.uint32), ref[0].view(np.uint32)) and np.array_equal(u8, ref[1])
-    assert (st["segments"], st["hits"]) == (ref[2]["segments"], ref[2]["hits"])
+    for mode in ("1", "2"):
+        monkeypatch.setenv("FR_BVH_STAGE", mode)
+        mean, u8, st = gpu.render(sc, sc.camera, w, h, spp, 8)
+        assert np.array_equal(mean.view(np.uint32), ref[0].view(np.uint32)) and np.array_equal(u8, ref[1])
+        assert (st["segments"], st["hits"]) == (ref[2]["segments"], ref[2]["hits"])
 
 
 def test_bvh_far_scene_axis_parallel_bounces(gpu, monkeypatch):
