@@ -5,11 +5,17 @@ trace kernel's mean HIP-event time per launch for each k, then a summary with th
 max over shards. The slowest shard bounds an N-GPU frame (bench.py reports the max over
 ranks), so DESIGN.md §6's predicted efficiency at N uses the max.
 
-    python tools/shard_stream.py N [K] [--shards k0,k1,...]
+    python tools/shard_stream.py N [K] [--shards k0,k1,...] [--orders fwd,rev,shuf]
 
-Default shards: all of 0..N-1. FR_FRAME_PIPE / FR_SCENE_JIT pass through (A/B knobs)."""
+Default shards: all of 0..N-1. FR_FRAME_PIPE / FR_SCENE_JIT pass through (A/B knobs).
+--orders runs the shard list once per order (fwd: as given, rev: reversed, shuf: a fixed
+shuffle) and ends with a table of each shard's time over the orders and of each run
+position's time over the orders: a slow shard that stays slow in every order is the shard's
+work; a slow first (or last) position whatever the shard is the box or the run order."""
 import json
 import os
+import random
+import statistics
 import sys
 import time
 
@@ -42,6 +48,7 @@ def stream_shard(sc, frame, n, k, frames, jit):
     return {"shards": n, "shard": k, "frames": frames, "ms_per_frame": round(ms, 4),
             "trace_ms_per_launch": round(sum(launches) / max(1, len(launches)), 4),
             "trace_launches": st["trace_launches"], "samples": st["samples"], "segments": st["segments"],
+            "hits": st["hits"], "scatters": st["scatters"],
             "pipe": os.environ.get("FR_FRAME_PIPE", ""), "occupancy": st["occupancy"]}
 
 
@@ -50,23 +57,42 @@ def main():
     n = int(args[0]) if args else 8
     frames = int(args[1]) if len(args) > 1 else 20
     shards = list(range(n))
+    orders = ["fwd"]
     for i, x in enumerate(sys.argv):
         if x == "--shards":
             shards = [int(v) for v in sys.argv[i + 1].split(",")]
+        if x == "--orders":
+            orders = sys.argv[i + 1].split(",")
     jit = os.environ.get("FR_SCENE_JIT") != "0"
     sc = fr.Scene.from_file(fr.scene_path("scene_08"), W, H)
     frame = fr.PinnedFrame(W, H)
-    rows = []
-    for k in shards:
-        r = stream_shard(sc, frame, n, k, frames, jit)
-        rows.append(r)
-        print(json.dumps(r), flush=True)
-    ms = [r["ms_per_frame"] for r in rows]
-    worst = max(rows, key=lambda r: r["ms_per_frame"])
-    print(json.dumps({"shards": n, "summary": True, "timed": [r["shard"] for r in rows],
-                      "ms_per_frame_min": min(ms), "ms_per_frame_max": max(ms),
-                      "slowest_shard": worst["shard"], "samples_total": sum(r["samples"] for r in rows)}),
-          flush=True)
+    by_shard, by_pos = {}, {}
+    for order in orders:
+        seq = list(shards)
+        if order == "rev":
+            seq.reverse()
+        elif order == "shuf":
+            random.Random(12345).shuffle(seq)
+        rows = []
+        for pos, k in enumerate(seq):
+            r = stream_shard(sc, frame, n, k, frames, jit)
+            r["order"], r["position"] = order, pos
+            rows.append(r)
+            by_shard.setdefault(k, []).append(r["ms_per_frame"])
+            by_pos.setdefault(pos, []).append(r["ms_per_frame"])
+            print(json.dumps(r), flush=True)
+        ms = [r["ms_per_frame"] for r in rows]
+        worst = max(rows, key=lambda r: r["ms_per_frame"])
+        print(json.dumps({"shards": n, "summary": True, "order": order, "timed": [r["shard"] for r in rows],
+                          "ms_per_frame_min": min(ms), "ms_per_frame_max": max(ms),
+                          "slowest_shard": worst["shard"], "samples_total": sum(r["samples"] for r in rows)}),
+              flush=True)
+    if len(orders) > 1:
+        med = lambda v: round(statistics.median(v), 4)  # noqa: E731
+        print(json.dumps({"shards": n, "orders": orders,
+                          "shard_median_ms": {k: med(v) for k, v in sorted(by_shard.items())},
+                          "shard_ms": {k: v for k, v in sorted(by_shard.items())},
+                          "position_median_ms": {p: med(v) for p, v in sorted(by_pos.items())}}), flush=True)
     frame.close()
 
 
