@@ -1422,16 +1422,29 @@ int fr_ctx_trace_log(fr_ctx* c, int enable) {
 }
 
 int fr_ctx_trace_log_read(fr_ctx* c, int which, double* ms, uint32_t cap, uint32_t* n) {
-  if (!c || !n || which < 0 || which > 1) return set_error(FR_EARG, "fr_ctx_trace_log_read: bad argument");
+  if (!c || !n || which < 0 || which > 3) return set_error(FR_EARG, "fr_ctx_trace_log_read: bad argument");
   SET_DEVICE(c->device);
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->stream2));
   HIPCHK(hipStreamSynchronize(c->stream_sum));  // a pipelined render's end event is recorded there
-  *n = static_cast<uint32_t>(c->log_n[which]);
-  for (size_t i = 0; i < c->log_n[which] && i < cap && ms; ++i) {
-    float t = 0.0f;
-    HIPCHK(hipEventElapsedTime(&t, c->log_ev[which][2 * i], c->log_ev[which][2 * i + 1]));
-    ms[i] = t;
+  // which 0 / 1: durations of the trace launches / renders; 2 / 3: their start and end times
+  // (two values each) from the first logged trace launch's start (a timeline)
+  const int w = which & 1;
+  *n = static_cast<uint32_t>(c->log_n[w]);
+  for (size_t i = 0; i < c->log_n[w] && ms; ++i) {
+    if (which < 2) {
+      if (i >= cap) break;
+      float t = 0.0f;
+      HIPCHK(hipEventElapsedTime(&t, c->log_ev[w][2 * i], c->log_ev[w][2 * i + 1]));
+      ms[i] = t;
+    } else {
+      if (2 * i + 1 >= cap || c->log_n[0] == 0) break;
+      float a = 0.0f, b = 0.0f;
+      HIPCHK(hipEventElapsedTime(&a, c->log_ev[0][0], c->log_ev[w][2 * i]));
+      HIPCHK(hipEventElapsedTime(&b, c->log_ev[0][0], c->log_ev[w][2 * i + 1]));
+      ms[2 * i] = a;
+      ms[2 * i + 1] = b;
+    }
   }
   return FR_OK;
 }

@@ -249,11 +249,101 @@ __global__ __launch_bounds__(kSumThreads) FR_SUM_VGPR_CAP void sum_kernel(KParam
   }
 }
 
+// 8-B records in full 16-sample slots (the headline's case), without the LDS tile: each
+// thread loads its own slot (128 B, eight 16-B loads; the wave's loads cover 64 consecutive
+// slots, 8 KB) into registers, the next block's slot while this one is summed. Beside the
+// next frame's trace this kernel runs one wave per SIMD: the tile's 64 LDS writes and reads
+// per thread and block, and its two barriers per block, were what it waited on there.
+// Same sums in the same order as sum_kernel<2, 0> (FR_SUM_DIRECT=0 selects that one).
+#ifndef FR_SUM_DIRECT
+#define FR_SUM_DIRECT 1
+#endif
+__global__ __launch_bounds__(kSumThreads) FR_SUM_VGPR_CAP void sum_nib_kernel(
+    KParams kp, const float* __restrict__ samples, float* __restrict__ running, float* __restrict__ out_mean,
+    uint8_t* __restrict__ out_u8, int first, int last, const float4* __restrict__ att, uint32_t n_prims) {
+  __shared__ float4 att16[16];  // level k's entry at byte 16 x nibble (15: the unit entry)
+  const uint32_t t = threadIdx.x;
+  if (t < 16u) {
+    const float4 a = t < n_prims ? att[t] : make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    att16[t] = make_float4(a.x, a.y, a.z, 0.0f);
+  }
+  const uint32_t q0 = blockIdx.x * kSumThreads, q = q0 + t;
+  const uint32_t nq = min(kSumThreads, kp.P - q0);
+  uint32_t x = 0, y = 0;
+  const bool valid = q < kp.P && slot_xy(kp, q, x, y);
+  V3 sum = (first || !valid) ? V3{0.0f, 0.0f, 0.0f} : V3{running[3 * q], running[3 * q + 1], running[3 * q + 2]};
+  asm volatile("" : "+v"(sum.x), "+v"(sum.y), "+v"(sum.z));
+  __syncthreads();
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  constexpr uint32_t kV = 2u * kBlockSamples / 4u;  // float4 per slot
+  // block bl's slots of this workgroup: one buffer resource (64-bit base, range = its slots),
+  // this thread's slot at a 32-bit lane offset; past the last slot the loads return 0
+  auto load = [&](uint32_t bl, v4f* v) {
+    const float* base = samples + 2u * (static_cast<size_t>(bl * kp.P + q0) * kBlockSamples);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base), 0, static_cast<int>(nq * kV * 16u), 0x00020000);
+#pragma unroll
+    for (uint32_t k = 0; k < kV; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, t * (kV * 16u) + k * 16u, 0, 0);
+  };
+  auto add_block = [&](uint32_t bl, const v4f* v) {
+    const uint32_t n = min(kBlockSamples, kp.spp - (kp.b0 + bl) * kBlockSamples);
+#pragma unroll
+    for (uint32_t j = 0; j < kBlockSamples; ++j) {
+      if (j < n) {
+        const float tf = (j & 1u) ? v[j >> 1].z : v[j >> 1].x;
+        const uint32_t w = __float_as_uint((j & 1u) ? v[j >> 1].w : v[j >> 1].y);
+        // the eight entries read before the first multiply: one wave per SIMD runs this
+        // beside the trace, and the reads' latency is then not hidden by other waves
+        const uint32_t w4 = w << 4;
+        float4 e[8];
+#pragma unroll
+        for (int k = 7; k >= 0; --k) {
+          const uint32_t off = (((k & 1) ? w : w4) >> (8 * (k >> 1))) & 0xF0u;
+          e[k] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(att16) + off);
+        }
+        V3 col = __float_as_uint(tf) == kDeferAbsorbed ? V3{0.0f, 0.0f, 0.0f} : sky_from_t(tf);
+#pragma unroll
+        for (int k = 7; k >= 0; --k) col = mul(V3{e[k].x, e[k].y, e[k].z}, col);
+        sum = add(sum, col);
+      }
+    }
+  };
+  v4f va[kV], vb[kV];
+  if (kp.nb) load(0, va);
+  for (uint32_t bl = 0; bl < kp.nb; bl += 2u) {
+    if (bl + 1u < kp.nb) load(bl + 1u, vb);
+    if (valid) add_block(bl, va);
+    if (bl + 1u >= kp.nb) break;
+    if (bl + 2u < kp.nb) load(bl + 2u, va);
+    if (valid) add_block(bl + 1u, vb);
+  }
+  if (!valid) return;
+  if (!last) {
+    running[3 * q] = sum.x;
+    running[3 * q + 1] = sum.y;
+    running[3 * q + 2] = sum.z;
+    return;
+  }
+  const size_t idx = (static_cast<size_t>(y) * kp.W + x) * 3u;
+  const V3 mean = divs(sum, static_cast<float>(kp.spp));  // tracer.rs:177
+  out_mean[idx + 0] = mean.x;
+  out_mean[idx + 1] = mean.y;
+  out_mean[idx + 2] = mean.z;
+  if (kp.flags & FR_FLAG_WRITE_U8) {
+    out_u8[idx + 0] = to_u8(mean.x);
+    out_u8[idx + 1] = to_u8(mean.y);
+    out_u8[idx + 2] = to_u8(mean.z);
+  }
+}
+
 hipError_t launch_sum(uint32_t wps, int kind, uint32_t blocks, hipStream_t stream, const KParams& kp,
                       const float* samples, float* running, float* out_mean, uint8_t* out_u8, int first, int last,
                       const float4* att, uint32_t n_prims) {
   const dim3 grid(blocks), block(kSumThreads);
-  if (wps == 2)
+  if (wps == 2 && FR_SUM_DIRECT && kp.ks == kBlockSamples && !(kp.flags & FR_FLAG_MT_BANDS))
+    hipLaunchKernelGGL(sum_nib_kernel, grid, block, 0, stream, kp, samples, running, out_mean, out_u8, first, last,
+                       att, n_prims);
+  else if (wps == 2)
     hipLaunchKernelGGL((sum_kernel<2, 0>), grid, block, 0, stream, kp, samples, running, out_mean, out_u8, first,
                        last, att, n_prims);
   else if (kind == 1)

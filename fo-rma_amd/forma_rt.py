@@ -534,14 +534,18 @@ class RenderContext:
         """Start (or stop) logging every trace-kernel launch's HIP-event duration."""
         check(lib().fr_ctx_trace_log(self._h, 1 if enable else 0))
 
-    def trace_log_read(self, frames=False):
+    def trace_log_read(self, frames=False, timeline=False):
         """HIP-event durations (ms) logged since trace_log(True): every trace-kernel launch,
-        or (frames=True) every whole render (trace + sum kernels)."""
-        which = 1 if frames else 0
+        or (frames=True) every whole render (trace + sum kernels). timeline=True: (start, end)
+        pairs instead, in ms from the first logged trace launch's start."""
+        which = (1 if frames else 0) + (2 if timeline else 0)
         n = C.c_uint32(0)
         check(lib().fr_ctx_trace_log_read(self._h, which, None, 0, C.byref(n)))
-        arr = (C.c_double * max(1, n.value))()
-        check(lib().fr_ctx_trace_log_read(self._h, which, arr, n.value, C.byref(n)))
+        k = 2 if timeline else 1
+        arr = (C.c_double * max(1, k * n.value))()
+        check(lib().fr_ctx_trace_log_read(self._h, which, arr, k * n.value, C.byref(n)))
+        if timeline:
+            return [(arr[2 * i], arr[2 * i + 1]) for i in range(n.value)]
         return [arr[i] for i in range(n.value)]
 
     def device_buffers(self):

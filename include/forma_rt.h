@@ -231,8 +231,10 @@ int fr_ctx_device_buffers(fr_ctx* ctx, float** d_mean_rgb, uint8_t** d_rgb8);
 /* Launch log: enable != 0 starts a new log (previous entries dropped); every later render
    records HIP events around each trace-kernel launch (on the launch's stream) and around
    the whole render (trace + sum kernels). _read waits for the logged work and writes up
-   to cap durations (ms) in order: which = 0 the trace launches, 1 the renders; *n = the
-   entries logged. Lets a caller streaming K frames average all K of them. */
+   to cap durations (ms) in order: which = 0 the trace launches, 1 the renders; which = 2
+   / 3 the same entries as (start, end) pairs in ms from the first logged trace launch's
+   start (2 values per entry, a timeline); *n = the entries logged. Lets a caller
+   streaming K frames average all K of them and see the gaps between them. */
 int fr_ctx_trace_log(fr_ctx* ctx, int enable);
 int fr_ctx_trace_log_read(fr_ctx* ctx, int which, double* ms, uint32_t cap, uint32_t* n);
 /* Everything a render of these parameters sets up before its first launch, without
