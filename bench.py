@@ -671,11 +671,11 @@ def run_rank(a, plan, torch, fr):
     my_samples = sum(s["samples"] for s in stats)
     total_samples = barrier.sum(my_samples)
     counts = {k: sum(s[k] for s in stats) / n for k in ("segments", "hits", "scatters", "samples")}
-    launches = max(1, stats[0]["trace_launches"])              # sample-block passes (DESIGN.md §4.5a)
+    launches = max(1, stats[0]["trace_launches"])              # sample-block passes (DESIGN.md §4.6)
     # means over all K frames from the launch log (not the last frame's events)
     kernel_ms = sum(frame_log) / max(1, len(frame_log))        # the render on its streams (trace + sum)
     launch_ms = sum(launch_log) / max(1, len(launch_log))      # what rocprof's average reports
-    # A small shard's consecutive traces overlap (the frame pipeline, DESIGN.md §4.5b): a
+    # A small shard's consecutive traces overlap (the frame pipeline, DESIGN.md §4.6): a
     # launch's own events then span part of its neighbour, so the roofline's kernel time is
     # capped at the step time (conservative).
     launch_ms_events = launch_ms
@@ -705,7 +705,7 @@ def run_rank(a, plan, torch, fr):
         "step": "render of the rank's strips + D2H gather of its f32 means and u8 image into pinned host memory",
         "host_sync": "each step" if a.sync_each else "after the K steps (frames streamed back to back)",
         # a frame's span, its trace's start to its sum's end: frames overlap under the frame
-        # pipeline (a frame's sum runs beside the next frames' traces, DESIGN.md §4.5b), so
+        # pipeline (a frame's sum runs beside the next frames' traces, DESIGN.md §4.6), so
         # this is longer than a step and no throughput follows from it
         "frame_span_ms": round(kernel_ms_max, 3),
         "segments_per_sample": round(total_segs / max(1.0, total_samples), 4),
@@ -744,7 +744,7 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # 20 frames (0.35 s of GPU time at N = 1): the frame pipeline's steady state, in which a
-    # frame's sum runs beside the next frame's trace (DESIGN.md §4.5b); the first and last
+    # frame's sum runs beside the next frame's trace (DESIGN.md §4.6); the first and last
     # frames' sums are inside the timed region too
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)

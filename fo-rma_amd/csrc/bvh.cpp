@@ -119,7 +119,7 @@ struct Builder {
     const uint32_t rl = build(begin, mid, depth + 1);
     const uint32_t rr = build(mid, end, depth + 1);
     BvhNode& nd = nodes[at];
-    // conservative padding (DESIGN.md §4.8)
+    // conservative padding (DESIGN.md §4.7)
     for (int k = 0; k < 3; ++k) {
       nd.a[k] = l.lo[k] - pad;
       nd.b[k] = l.hi[k] + pad;

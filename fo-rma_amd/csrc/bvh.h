@@ -1,4 +1,4 @@
-// Bounding volume hierarchy over a scene's primitives (DESIGN.md §4.8).
+// Bounding volume hierarchy over a scene's primitives (DESIGN.md §4.7).
 //
 // A binary BVH whose nodes carry both children's boxes ("child boxes in the parent"):
 // one 64-B fetch gives a lane two independent box tests; it steps into the nearer child

@@ -7,7 +7,7 @@
 // z = +-35, ...) compute the same slab distance from the same inputs; with the records as
 // literals the compiler sees that and computes each distinct (coordinate - o) * inv once
 // per segment. The tests, their order and their arithmetic are the list loop's, so the
-// image is the same bits (tests/test_gpu_parity.py::test_scene_jit_*). DESIGN.md §4.11.
+// image is the same bits (tests/test_gpu_parity.py::test_scene_jit_*). DESIGN.md §4.8.
 //
 // Where the code comes from (one code object per key, shared by every device of an arch):
 //   1. this process's code cache (built or read earlier; a module per device on top);

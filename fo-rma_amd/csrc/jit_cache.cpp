@@ -1,4 +1,4 @@
-// jit_cache.cpp — see jit_cache.h. DESIGN.md §4.11 (disk cache).
+// jit_cache.cpp — see jit_cache.h. DESIGN.md §4.8 (disk cache).
 #include "jit_cache.h"
 
 #include <stdio.h>

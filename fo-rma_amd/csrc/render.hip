@@ -408,7 +408,7 @@ struct fr_ctx {
   // [0..3] counters, [4..] diagnostics; [31] queue head: one set of 32 per frame slot
   unsigned long long* d_cnt = nullptr;
   unsigned long long* last_cnt = nullptr;  // the last render's set
-  // Frame pipeline (FR_FRAME_PIPE, DESIGN.md §4.5b): one-pass frames alternate between two
+  // Frame pipeline (FR_FRAME_PIPE, DESIGN.md §4.6): one-pass frames alternate between two
   // frame slots (sample buffer half, counter set), so frame k+1's trace starts when frame k's
   // trace ends while frame k's sum runs beside it; ev_fslot[s] = the end of the last sum
   // that used slot s, which the next frame on that slot waits for.
@@ -867,7 +867,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   // FR_PIPELINE (default 1) asks for at least that many passes; the buffer budget
   // (FR_SAMPLE_BUFFER_GB) may force more. Two pipelined passes measured 0.6 % faster
   // on C3, but overlapping launches blur each launch's own HIP-event time (DESIGN.md
-  // §4.5a), so one pass is the default.
+  // §4.6), so one pass is the default.
   // sample slots per item: a frame of spp < 16 (update()'s 1-spp frames) needs only spp
   kp.ks = p->spp < kBlockSamples ? (p->spp ? p->spp : 1u) : kBlockSamples;
   const bool small_depth = p->max_depth <= kSmallDepth && dc->n < 65536u;
@@ -910,14 +910,14 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   const int passes = nb_pass ? static_cast<int>((nblocks + nb_pass - 1) / nb_pass) : 0;
   // frame pipeline (fr_ctx::frame_slot): one-pass frames whose sample buffer fits twice
   // (FR_FRAME_PIPE=0 turns it off). Streamed scene_08 frames, shard 0 of N on one MI355X:
-  // 17.01 -> 16.59 ms at N = 1, 2.52 -> 2.29 ms at N = 8 (DESIGN.md §4.5b)
+  // 17.01 -> 16.59 ms at N = 1, 2.52 -> 2.29 ms at N = 8 (DESIGN.md §4.6)
   // Traces: frame k+1's trace follows frame k's on one stream, or, for a shard with fewer
   // than two pixel slots per grid lane (two items per lane and block or fewer: the queue's
   // drain is a large part of the frame, shards 0 of 4 and of 8), consecutive frames' traces
   // alternate between two streams, so the next frame's trace fills the CUs the previous
   // one's drain leaves idle: shard 0/8 2.47 -> 2.29 ms per frame, 0/4 4.27-4.46 -> 4.28
   // (steadier), the same at N = 1 and 2, where serial traces keep each launch's own event
-  // time (DESIGN.md §4.5b). FR_FRAME_PIPE=1 / 2 forces serial / overlapping traces.
+  // time (DESIGN.md §4.6). FR_FRAME_PIPE=1 / 2 forces serial / overlapping traces.
   // Two slots (FR_FRAME_SLOTS=3 or 4 asks for more when the budget holds them). With round
   // 3's sum, which ran longer than the trace beside it, three slots let frame k + 2's trace
   // start before frame k's sum ended; since round 4's sum keeps pace, two are faster (C3
@@ -1097,7 +1097,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       // pipelined frames leave room on every CU for the previous frame's sum workgroups:
       // one slot, or two for shards whose traces overlap (N >= 4: each frame's sum is then
       // short enough that the trace does better with it out of its way; shard 1/8 2.23 ->
-      // 2.18 ms per frame, 1/4 4.25 -> 4.19; at N = 1 two cost 6 %, DESIGN.md §4.5b)
+      // 2.18 ms per frame, 1/4 4.25 -> 4.19; at N = 1 two cost 6 %, DESIGN.md §4.6)
       if (fpipe) {
         const char* r = getenv("FR_FRAME_PIPE_RESERVE");
         grid.reserve = r ? static_cast<uint32_t>(atoi(r)) : fpipe_overlap ? 2u : 1u;

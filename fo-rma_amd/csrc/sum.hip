@@ -26,7 +26,7 @@ static_assert(kSumThreads % 64u == 0 && kSumThreads <= kDeferUnit + 1u, "whole w
 // here from a 12-B-per-entry attenuation table (tile + table fit three workgroups per CU).
 // WPS = 2: 8-B records {t, 4-bit winners} (KF_NIBBLE).
 
-// FR_SUM_VGPR_CAP: the sum runs beside seven trace workgroups per CU (DESIGN.md §4.5b),
+// FR_SUM_VGPR_CAP: the sum runs beside seven trace workgroups per CU (DESIGN.md §4.6),
 // whose 56 VGPRs per wave leave 120 per SIMD lane for one sum wave
 #ifndef FR_SUM_VGPRS
 #define FR_SUM_VGPRS 120
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kSumThreads) FR_SUM_VGPR_CAP void sum_kernel(KParam
 #ifndef FR_SUM_PRIO
 #define FR_SUM_PRIO 0
 #endif
-  // Pipelined frames (DESIGN.md §4.5b) run this kernel on the CU slot the next frame's
+  // Pipelined frames (DESIGN.md §4.6) run this kernel on the CU slot the next frame's
   // trace leaves free, where it takes about as long as the trace. A raised wave priority
   // slowed the trace by more than it sped the sum (FR_SUM_PRIO=3: C3 streamed 16.65 ->
   // 17.07 ms per frame in round 3; 1: 16.26 -> 16.73 in round 4): not used.

@@ -4,7 +4,7 @@
 // Compiled twice: into libforma_rt.so by hipcc (every specialisation, render.hip), and
 // at run time by hiprtc for a scene-specialised list kernel (FR_JIT_N defined: the
 // closest-hit list walk becomes an unrolled sequence of tests on the scene's records
-// as compile-time constants, jit.cpp; DESIGN.md §4.11). Everything here must therefore
+// as compile-time constants, jit.cpp; DESIGN.md §4.8). Everything here must therefore
 // compile under hiprtc: no host-only headers.
 #pragma once
 #if !defined(__HIPCC_RTC__)
@@ -60,7 +60,7 @@ constexpr uint32_t kMaxWgPerCu = 8;   // 2048 threads per CU / kBlock: the persi
 // ... for the 8-B-record kernels (scenes of <= 15 primitives, the headline's): measured
 // C3 trace 20.81 -> 20.69 ms at 6 (7 and 8 the same within noise); 6 on the other kernels
 // cost C2 +1.7 % and a 10k-sphere BVH frame +1.2 %, so they keep FR_KREJ
-// Re-tuned for the scene-specialised kernel (round 3, DESIGN.md §4.11): 9 with
+// Re-tuned for the scene-specialised kernel (round 3, DESIGN.md §4.8): 9 with
 // FR_CLAIM_MIN_NIB 3 streams C3 at 16.49 ms per frame against 16.63 (6 / 2), three runs;
 // shard 0/8 unchanged (tools/gpu_knob_shards.sh, profiles/r03k_knob_shards.log)
 #ifndef FR_KREJ_NIB
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #define FR_TRACE_PRIO 0
 #endif
   // FR_TRACE_PRIO (A/B): the trace's waves issue ahead of a concurrently running sum_kernel
-  // (the frame pipeline, DESIGN.md §4.5b), which then only takes the issue slots the trace
+  // (the frame pipeline, DESIGN.md §4.6), which then only takes the issue slots the trace
   // leaves idle
   if (FR_TRACE_PRIO) __builtin_amdgcn_s_setprio(FR_TRACE_PRIO);
   extern __shared__ uint32_t lds[];
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         // least (t, index) of the run below `closest`: a primitive listed before the
         // current winner may take an exact tie, tested with t_max one ulp above
         // closest. Boxes are padded, so no primitive the list loop accepts is culled
-        // (DESIGN.md §4.8). A lane steps into the nearer entered child and stacks the
+        // (DESIGN.md §4.7). A lane steps into the nearer entered child and stacks the
         // other; lanes that reach a leaf wait for the wave's others, so leaves are
         // tested together.
         typedef __attribute__((address_space(4))) const uint32_t cu32;

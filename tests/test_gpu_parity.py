@@ -531,7 +531,7 @@ def test_streamed_frames_match_the_oracle(gpu, shard, pipe, monkeypatch):
     streams alone order the frames, so the host frame holds the last frame's strips
     exactly, and the counters are that frame's. pipe "1": the frame pipeline (FR_FRAME_PIPE,
     frame k+1's trace beside frame k's sum); "2": consecutive traces may overlap too; "":
-    the default choice (DESIGN.md §4.5b)."""
+    the default choice (DESIGN.md §4.6)."""
     monkeypatch.setenv("FR_FRAME_PIPE", pipe)
     w, h, spp, depth = 64, 40, 20, 8
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
@@ -676,7 +676,7 @@ def test_c3_headline_frame_in_full(gpu):
     2,073,600 pixels (530.8 M samples) compared — means within 1e-5 and bit for bit, u8
     identical — and the whole-frame segment, hit and scatter counters equal. Both trace
     kernels: the compiled-in one and the scene-specialised one bench.py runs (DESIGN.md
-    §4.11)."""
+    §4.8)."""
     name, w, h, spp, depth = "scene_08", 1920, 1080, 256, 8
     sc = gpu.Scene.from_file(gpu.scene_path(name), w, h)
     runs = [gpu.render(sc, sc.camera, w, h, spp, depth, scene_jit=jit) for jit in (False, "wait")]
@@ -756,7 +756,7 @@ def test_c4_full_frame_every_shard_through_mctx(gpu, monkeypatch):
     assert np.array_equal(mean[:, ::8].view(np.uint32), cmean[:, ::8].view(np.uint32))
 
 
-# ---- BVH (scenes of >= 48 primitives, <= 32 planes; DESIGN.md §4.8) -------------
+# ---- BVH (scenes of >= 48 primitives, <= 32 planes; DESIGN.md §4.7) -------------
 
 def bvh_cost(prims):
     """bvh.cpp's weighted test cost (the BVH is used at >= 48, with >= 48 primitives)."""

@@ -1,5 +1,5 @@
 // pk_rate.hip — issue rate of packed vs plain f32 VALU ops on gfx950 (a microbenchmark for
-// DESIGN.md §4.7b): every wave runs N iterations of 16 independent instructions of one
+// profiles/AB_LOG.md): every wave runs N iterations of 16 independent instructions of one
 // kind; the kernel's time gives wave-instructions per SIMD-cycle.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
