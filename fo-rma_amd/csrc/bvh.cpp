@@ -104,9 +104,34 @@ struct Builder {
   // Reference to the subtree over items[begin, end) at depth `depth`.
   uint32_t build(uint32_t begin, uint32_t end, uint32_t depth) {
     const uint32_t n = end - begin;
-    if (n <= leaf_max) return bvh_leaf_ref(slot_base + begin, n);
+    // FR_BVH_CT = c (A/B): SAH termination with a node step costing c primitive tests: a node
+    // of at most FR_BVH_LEAF_CAP (8) primitives becomes a leaf when testing them all costs no
+    // more than the best split (c + the children's area-weighted counts); off: every node
+    // of at most leaf_max primitives is a leaf and every larger one is split
+    static const double ct = [] {
+      const char* e = getenv("FR_BVH_CT");
+      return e ? atof(e) : -1.0;
+    }();
+    static const uint32_t leaf_cap = [] {
+      const char* e = getenv("FR_BVH_LEAF_CAP");
+      const int v = e ? atoi(e) : 8;
+      return static_cast<uint32_t>(v >= 1 && v <= static_cast<int>(kBvhLeafCountMax) ? v : 8);
+    }();
+    if (ct < 0.0 && n <= leaf_max) return bvh_leaf_ref(slot_base + begin, n);
     Box3 cbox;
     const Box3 box = bounds(begin, end, &cbox);
+    if (ct >= 0.0 && n <= std::max(leaf_cap, leaf_max)) {
+      if (n == 1) return bvh_leaf_ref(slot_base + begin, n);
+      double best = INFINITY;
+      for (int k = 0; k < 3; ++k) {
+        if (!(cbox.hi[k] - cbox.lo[k] > 0.0f)) continue;
+        double c = INFINITY;
+        sweep_split(begin, end, k, &c);
+        best = std::min(best, c);
+      }
+      const double a = box.area();
+      if (!(a > 0.0) || a * n <= ct * a + best) return bvh_leaf_ref(slot_base + begin, n);
+    }
     // SAH while the subtree can still be finished below the cap by balanced splits
     // (a median split at depth d with d + levels(n) = kBvhStack leaves the deepest
     // internal node at kBvhStack - 1)
