@@ -533,8 +533,8 @@ static std::string jit_defines() {
 #ifdef FR_SPHERE_IEEE
   d += "#define FR_SPHERE_IEEE\n";
 #endif
-#ifdef FR_FAST_SKY
-  d += "#define FR_FAST_SKY\n";
+#ifdef FR_SKY_IEEE
+  d += "#define FR_SKY_IEEE\n";
 #endif
 #ifdef FR_NO_UNROLL_NIB
   d += "#define FR_NO_UNROLL_NIB\n";

@@ -1207,7 +1207,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           sky_dy = d.y;
           tsky = __float_as_uint(d.x * d.x + d.y * d.y + d.z * d.z);  // length()'s sum, in its order
         } else if (DEFER)
-#ifdef FR_FAST_SKY
+#ifndef FR_SKY_IEEE
+          // the sqrt and division by their core sequences under a range guard (sky_t_fast,
+          // bit-identical): C3 frame 15.52 -> 15.27 ms (in round 3, before the sum ran beside
+          // the trace, it had measured neutral); FR_SKY_IEEE builds the compiler's sequences
           tsky = __float_as_uint(sky_t_fast(d));  // tracer.rs:211-218, the blend in sum_kernel
 #else
           tsky = __float_as_uint(sky_t(d));  // tracer.rs:211-218, the blend in sum_kernel

@@ -147,10 +147,11 @@ def test_guarded_recip_and_jitter_division(gpu):
 
 
 def test_fast_sky_parameter_is_bit_identical(gpu):
-    """sky_t_fast (the sky blend parameter with guarded core sqrt/division sequences,
-    render.hip FR_FAST_SKY) against the plain correctly rounded sky_t on the device, bit for
-    bit (op 14 returns the XOR of both results' bits), over random directions of every scale
-    and the guards' edges: tiny, zero, -0, denormal and huge components."""
+    """sky_t_fast (the sky blend parameter with guarded core sqrt/division sequences, the
+    trace kernel's default; FR_SKY_IEEE builds the plain one) against the plain correctly
+    rounded sky_t on the device, bit for bit (op 14 returns the XOR of both results' bits),
+    over random directions of every scale and the guards' edges: tiny, zero, -0, denormal
+    and huge components."""
     import ctypes as C
     rng = np.random.default_rng(14)
     fp = C.POINTER(C.c_float)
