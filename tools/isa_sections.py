@@ -9,7 +9,7 @@ are counted (v_* opcodes; SALU, LDS and memory instructions separately).
 Dynamic side: an FR_SECCNT build of the library counts how many times a wave enters each
 region per launch (the FR_SECCNT line on stderr, captured on the GPU box).
 
-    python tools/isa_sections.py isa [--template=1,0,9,8,0,0,2,1] [--nojit] [-DNAME=V]  -> static table (JSON)
+    python tools/isa_sections.py isa [--template=1,0,9,8,0,0,2,1] [--nojit] [--scene=scene_08] [--prelude=FILE] [-DNAME=V]  -> static table (JSON)
       (--nojit: the compiled-in kernel, e.g. --template=2,0,4,8,1,0,0,1 --nojit for C5's BVH kernel)
     python tools/isa_sections.py combine STATIC.json SECCNT_LINE_FILE SEGMENTS VALU_MEASURED [GRABS]
 
@@ -37,31 +37,43 @@ OPTS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fhip-fp32-
         "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize"]
 
 
-def scene08_records():
+def scene_records(name="scene_08"):
+    """The scene's 64-B device records as render.hip upload_scene lays them out (spheres,
+    boxes and planes; the kind in g3.w)."""
     sys.path.insert(0, os.path.join(ROOT, "fo-rma_amd"))
     import forma_rt as fr
-    sc = fr.Scene.from_file(fr.scene_path("scene_08"), 64, 36)
+    sc = fr.Scene.from_file(fr.scene_path(name), 64, 36)
     words = []
     for p in sc.prims():
-        g = list(p.g[:6])
-        rec = list(struct.unpack("16I", struct.pack("16f", g[0], g[1], g[2], 0, g[3], g[4], g[5], 0, *([0.0] * 8))))
-        rec[15] = 2  # FR_AABB in g3.w (render.hip upload_scene)
+        g = list(p.g)
+        if p.kind == fr.FR_SPHERE:
+            f = g[0:4] + [0.0] * 12
+        elif p.kind == fr.FR_AABB:
+            f = g[0:3] + [0.0] + g[3:6] + [0.0] * 9
+        elif p.kind == fr.FR_PLANE:
+            f = g[0:3] + [0.0] + g[3:6] + [0.0] + g[6:9] + [0.0] * 5
+        else:
+            raise SystemExit(f"isa_sections: kind {p.kind} not laid out here")
+        rec = list(struct.unpack("16I", struct.pack("16f", *f)))
+        rec[15] = p.kind
         words.append(rec)
     return words
 
 
-def build_isa(targs, extra_defs=(), jit=True):
+def build_isa(targs, extra_defs=(), jit=True, scene="scene_08", prelude_file=None):
     out = os.path.join(ROOT, "fo-rma_amd", "build", "isa_jit")
     os.makedirs(out, exist_ok=True)
     pre = "".join(f"#define {k} {v}\n" for k, v in DEFINES.items())
     if jit:  # the scene-specialised build (scene_08's records); else the compiled-in kernel
-        recs = scene08_records()
+        recs = scene_records(scene)
         pre += f"#define FR_JIT_N {len(recs)}u\n#define FR_JIT_REC " + ",".join(
             "{" + ",".join(f"0x{w:08x}u" for w in r) + "}" for r in recs) + "\n"
+    if prelude_file:  # e.g. the FR_JIT_CLU_* cluster constants render.hip adds for a scene
+        pre += open(prelude_file).read()
     ta = targs
     inst = (f"template __global__ void fr::trace_kernel<{ta[0]}, {'true' if ta[1] else 'false'}, {ta[2]}, {ta[3]}, "
             f"{'true' if ta[4] else 'false'}, {'true' if ta[5] else 'false'}, {ta[6]}, {ta[7]}>(fr::KArgs);\n")
-    src = os.path.join(out, "scene08_kernel.hip" if jit else "kernel_%s.hip" % "_".join(map(str, targs)))
+    src = os.path.join(out, (scene.replace("_", "") + "_kernel.hip") if jit else "kernel_%s.hip" % "_".join(map(str, targs)))
     with open(src, "w") as f:
         f.write(pre + '#include "trace_kernel.h"\n' + inst)
     asm = src[:-4] + ".s"
@@ -176,14 +188,20 @@ if __name__ == "__main__":
         targs = [1, 0, 9, 8, 0, 0, 2, 1]
         extra = []
         jit = True
+        scene = "scene_08"
+        prelude_file = None
         for a in sys.argv[2:]:
             if a.startswith("--template="):
                 targs = [int(x) for x in a.split("=", 1)[1].split(",")]
             elif a == "--nojit":
                 jit = False
+            elif a.startswith("--scene="):
+                scene = a.split("=", 1)[1]
+            elif a.startswith("--prelude="):
+                prelude_file = a.split("=", 1)[1]
             elif a.startswith("-D"):
                 extra.append(a)
-        asm = build_isa(targs, extra, jit)
+        asm = build_isa(targs, extra, jit, scene, prelude_file)
         tab, meta = count_regions(asm)
         print(json.dumps({"template": targs, "asm": os.path.relpath(asm, ROOT), "meta": meta, "regions": tab},
                          indent=1))
