@@ -413,7 +413,8 @@ def test_multi_context_matches_one_device_bit_for_bit(gpu, n, jit):
 
 def test_launch_log_times_every_launch(gpu, monkeypatch):
     """fr_ctx_trace_log: HIP-event durations of every trace launch and every render across
-    streamed frames (bench.py averages them), here with two passes per frame."""
+    streamed frames (bench.py averages them), here with two passes per frame, and the same
+    events as a timeline (tools/frame_gaps.py)."""
     monkeypatch.setenv("FR_PIPELINE", "2")
     w, h = 64, 40
     sc = gpu.Scene.from_file(gpu.scene_path("scene_08"), w, h)
@@ -430,6 +431,15 @@ def test_launch_log_times_every_launch(gpu, monkeypatch):
     assert len(launches) == 6 and len(frames) == 3
     assert all(t > 0 for t in launches) and all(f >= 0.5 * (a + b) for f, a, b in zip(frames, launches[::2],
                                                                                       launches[1::2]))
+    # the same entries as a timeline (which 2 / 3): (start, end) from the first launch's
+    # start; each pair's length is the duration above, launches and frames in order
+    tl, ftl = ctx.trace_log_read(timeline=True), ctx.trace_log_read(frames=True, timeline=True)
+    assert len(tl) == 6 and len(ftl) == 3 and tl[0][0] == 0.0
+    for (a, b), dur in zip(tl, launches):
+        assert b >= a and abs((b - a) - dur) <= 1e-3 * max(1.0, dur)
+    for i in range(3):  # a render's span holds both of its passes
+        passes = tl[2 * i:2 * i + 2]
+        assert ftl[i][0] <= min(a for a, _ in passes) + 1e-3 and ftl[i][1] >= max(b for _, b in passes) - 1e-3
     ctx.trace_log(False)
     ctx.render(sc, sc.camera, p)
     ctx.sync()

@@ -105,6 +105,9 @@ def test_generator_scene_bvh_build_clean(exe, tmp_path):
     (r,) = _run(exe, "json", str(p))
     assert r["rc"] == FR_OK and r["prims"] == 10000
     assert r["bvh"]["ok"] == 1 and r["bvh"]["order"] == 10000
+    # the full-sweep SAH tree (bvh.cpp): internal nodes below the stack's 16 levels (the
+    # launch sizes its LDS stack to depth + 1 levels), leaves of at most 4 spheres
+    assert r["bvh"]["depth"] < 16 and 10000 / 4 - 1 <= r["bvh"]["nodes"] < 10000
 
 
 def test_malformed_json_corpus_fails_cleanly(exe, tmp_path):
