@@ -5,7 +5,7 @@ trace kernel's mean HIP-event time per launch for each k, then a summary with th
 max over shards. The slowest shard bounds an N-GPU frame (bench.py reports the max over
 ranks), so DESIGN.md §6's predicted efficiency at N uses the max.
 
-    python tools/shard_stream.py N [K] [--shards k0,k1,...] [--orders fwd,rev,shuf]
+    python tools/shard_stream.py N [K] [--shards k0,k1,...] [--orders fwd,rev,shuf] [--warm W]
 
 Default shards: all of 0..N-1. FR_FRAME_PIPE / FR_SCENE_JIT pass through (A/B knobs).
 --orders runs the shard list once per order (fwd: as given, rev: reversed, shuf: a fixed
@@ -26,11 +26,11 @@ import forma_rt as fr  # noqa: E402
 W, H, SPP, DEPTH = 1920, 1080, 256, 8
 
 
-def stream_shard(sc, frame, n, k, frames, jit):
+def stream_shard(sc, frame, n, k, frames, jit, warm=2):
     p = fr.make_params(W, H, SPP, DEPTH, shard_index=k, shard_count=n, scene_jit=jit)
     ctx = fr.RenderContext(0)
     ctx.prepare(sc, sc.camera, p)
-    for _ in range(2):
+    for _ in range(warm):
         ctx.render(sc, sc.camera, p)
         ctx.download_async(frame)
     ctx.wait()
@@ -58,7 +58,10 @@ def main():
     frames = int(args[1]) if len(args) > 1 else 20
     shards = list(range(n))
     orders = ["fwd"]
+    warm = 2
     for i, x in enumerate(sys.argv):
+        if x == "--warm":
+            warm = int(sys.argv[i + 1])
         if x == "--shards":
             shards = [int(v) for v in sys.argv[i + 1].split(",")]
         if x == "--orders":
@@ -75,7 +78,7 @@ def main():
             random.Random(12345).shuffle(seq)
         rows = []
         for pos, k in enumerate(seq):
-            r = stream_shard(sc, frame, n, k, frames, jit)
+            r = stream_shard(sc, frame, n, k, frames, jit, warm)
             r["order"], r["position"] = order, pos
             rows.append(r)
             by_shard.setdefault(k, []).append(r["ms_per_frame"])
