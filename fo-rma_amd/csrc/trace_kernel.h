@@ -602,7 +602,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   uint32_t sbest = 0, s = 0, s_end = 0, nseg = 0, nhit = 0;  // (scatters = segments - samples: the host's)
   // (a sample's index within its block is s mod kBlockSamples: blocks start at multiples of it)
   static_assert((kBlockSamples & (kBlockSamples - 1u)) == 0u, "blocks of a power-of-two sample count");
-  uint32_t jfirst = 0;       // kStageSpansSub: the item's first sample in the block
   V3 pend{0.0f, 0.0f, 0.0f};  // RSTG: the pair's first colour (an even jj)
 #ifdef FR_DIAG
   uint32_t diag_tb = 0, diag_seg0 = 0;  // the item's batch index, segments at its claim
@@ -759,7 +758,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           const uint32_t k = (b >> 28) & 3u;
           const bool fine = (b & kFineKey) != 0u;
           const uint32_t j0 = k * kFineSamples;
-          if (kStageSpansSub) jfirst = j0;
           s = (b & 0x0FFFFFFFu) * kBlockSamples + j0;
           out = kw.samples + WPS * (static_cast<size_t>(item - k * kp.P) * kp.ks);
 #ifdef FR_DIAG
@@ -1391,7 +1389,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         if (full || s + 1u == s_end) {
           const uint32_t g0 = jj & ~(STG - 1u);
           // (a sub-block inside a wider group stores from its own first sample)
-          const uint32_t lo = kStageSpansSub ? max(g0, jfirst) : g0;
+          // (its first sample: items of block b_fine are the 4-aligned sub-blocks, derived
+          // here rather than held in a register through the loop)
+          const bool fine_item = kStageSpansSub && kp.b_fine != 0u && s / kBlockSamples == kp.b_fine;
+          const uint32_t lo = fine_item ? (jj & ~(kFineSamples - 1u)) : g0;
           float* dst = out + WPS * g0;
           if (full && kp.ks == kBlockSamples && lo == g0) {
             if constexpr ((WPS * STG) % 4u == 0u) {

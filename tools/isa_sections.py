@@ -63,7 +63,11 @@ def scene_records(name="scene_08"):
 def build_isa(targs, extra_defs=(), jit=True, scene="scene_08", prelude_file=None):
     out = os.path.join(ROOT, "fo-rma_amd", "build", "isa_jit")
     os.makedirs(out, exist_ok=True)
-    pre = "".join(f"#define {k} {v}\n" for k, v in DEFINES.items())
+    defs = dict(DEFINES)
+    for a in extra_defs:  # -DNAME=V overrides the host build's value of NAME
+        if a.startswith("-D") and "=" in a and a[2:].split("=", 1)[0] in defs:
+            defs[a[2:].split("=", 1)[0]] = a.split("=", 1)[1]
+    pre = "".join(f"#define {k} {v}\n" for k, v in defs.items())
     if jit:  # the scene-specialised build (scene_08's records); else the compiled-in kernel
         recs = scene_records(scene)
         pre += f"#define FR_JIT_N {len(recs)}u\n#define FR_JIT_REC " + ",".join(
@@ -77,6 +81,7 @@ def build_isa(targs, extra_defs=(), jit=True, scene="scene_08", prelude_file=Non
     with open(src, "w") as f:
         f.write(pre + '#include "trace_kernel.h"\n' + inst)
     asm = src[:-4] + ".s"
+    extra_defs = [a for a in extra_defs if not (a.startswith("-D") and "=" in a and a[2:].split("=", 1)[0] in defs)]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-I", CSRC, "-I",
            os.path.join(ROOT, "include"), *OPTS, "-DFR_SEC_MARKS", *extra_defs, src, "-o", asm]
     subprocess.run(cmd, check=True)
