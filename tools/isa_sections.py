@@ -14,7 +14,8 @@ region per launch (the FR_SECCNT line on stderr, captured on the GPU box).
     python tools/isa_sections.py combine STATIC.json SECCNT_LINE_FILE SEGMENTS VALU_MEASURED [GRABS]
 
 combine multiplies the two: VALU instructions per region per launch, their share, and the
-lane-slots per segment (x 64 / segments)."""
+lane-slots per segment (x 64 / segments). ISA_NOMARKS=1 compiles without the markers (the
+product kernel's exact registers: the markers' asm statements can change allocation)."""
 import json
 import os
 import re
@@ -83,7 +84,8 @@ def build_isa(targs, extra_defs=(), jit=True, scene="scene_08", prelude_file=Non
     asm = src[:-4] + ".s"
     extra_defs = [a for a in extra_defs if not (a.startswith("-D") and "=" in a and a[2:].split("=", 1)[0] in defs)]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-I", CSRC, "-I",
-           os.path.join(ROOT, "include"), *OPTS, "-DFR_SEC_MARKS", *extra_defs, src, "-o", asm]
+           os.path.join(ROOT, "include"), *OPTS, *([] if os.environ.get("ISA_NOMARKS") else ["-DFR_SEC_MARKS"]),
+           *extra_defs, src, "-o", asm]
     subprocess.run(cmd, check=True)
     return asm
 
