@@ -845,6 +845,32 @@ def test_bvh_matches_list_order_loop(gpu, seed, planes, depth, monkeypatch):
     assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
 
 
+@pytest.mark.parametrize("layout", ["same", "line", "pairs"])
+def test_bvh_degenerate_trees_keep_list_order_ties(gpu, layout, monkeypatch):
+    """Trees the SAH sweep cannot separate: 64 identical spheres (every hit a tie: the list's
+    first wins), 64 spheres on one line, and 32 pairs of coincident spheres of different
+    colours. The BVH walk against the oracle and the in-order loop, bit for bit."""
+    w, h, spp, depth = 40, 24, 3, 8
+    r = np.random.default_rng(11)
+    prims = []
+    for i in range(64):
+        c = {"same": (0.0, 0.0, -3.0), "line": (0.3 * i - 9.6, 0.0, -6.0),
+             "pairs": tuple(r.uniform(-3, 3, 2)) + (-7.0,) if i % 2 == 0 else None}[layout]
+        if c is None:
+            c = prims[-1]["g"][:3]  # the pair's second sphere: the same centre
+        prims.append(S.sphere(tuple(float(v) for v in c), 0.6, i % 4, tuple(float(v) for v in r.uniform(0.2, 1, 3)), 0.1))
+    prims.append(S.sphere((0.0, -100.5, -1.0), 100.0, 0, (0.5, 0.5, 0.5), 0.0))
+    assert bvh_cost(prims) >= 48 and len(prims) >= 48
+    sc = gpu.Scene.from_prims(prims)
+    cam, ocam = gpu.camera_new(w, h), O.camera_new(w, h)
+    mean, u8, st = gpu.render(sc, cam, w, h, spp, depth, seed=5)
+    omean, ou8, ocnt, _ = O.render(prims, ocam, w, h, spp, depth, seed=5, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    monkeypatch.setenv("FR_BVH", "0")
+    mean0, _, st0 = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=5)
+    assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
+
+
 def test_bvh_far_origins_from_stale_plane_records(gpu, monkeypatch):
     """Planes listed after the other primitives, small and in every orientation: a plane
     whose denominator gate passes (plane.rs:26) but whose bounds test fails still writes

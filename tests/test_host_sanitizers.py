@@ -110,6 +110,30 @@ def test_generator_scene_bvh_build_clean(exe, tmp_path):
     assert r["bvh"]["depth"] < 16 and 10000 / 4 - 1 <= r["bvh"]["nodes"] < 10000
 
 
+def test_degenerate_bvh_inputs_build_clean(exe, tmp_path):
+    """The full-sweep SAH builder on degenerate lists: 200 identical spheres (every centroid
+    and box equal: no split separates, median splits by list order), and 200 spheres on one
+    line (one axis with extent, two without). Builds clean, every primitive in the leaf
+    order once, internal nodes below the 16 stack levels."""
+    import copy
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_scene", os.path.join(ROOT, "tools", "gen_scene.py"))
+    gs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gs)
+    base = json.loads(gs.dumps(gs.generator_scene(200, "sphere")))
+    paths = []
+    for name, pos in (("same", lambda i: (1.0, 2.0, 3.0)), ("line", lambda i: (0.25 * i, 0.0, 0.0))):
+        d = copy.deepcopy(base)
+        for i, o in enumerate(d["objects"]):
+            o["position"] = dict(zip("xyz", pos(i)))
+        p = tmp_path / f"{name}.json"
+        p.write_text(json.dumps(d))
+        paths.append(str(p))
+    for r in _run(exe, "json", *paths):
+        assert r["rc"] == FR_OK and r["prims"] == 200, r
+        assert r["bvh"]["ok"] == 1 and r["bvh"]["order"] == 200 and r["bvh"]["depth"] < 16, r
+
+
 def test_malformed_json_corpus_fails_cleanly(exe, tmp_path):
     paths = _malformed_corpus(str(tmp_path))
     res = _run(exe, "json", *paths)
