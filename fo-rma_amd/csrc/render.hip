@@ -515,6 +515,7 @@ static std::string jit_defines() {
   def("FR_FINE_SAMPLES", FR_FINE_SAMPLES);
   def("FR_STAGE", FR_STAGE);
   def("FR_BVH_STAGE", FR_BVH_STAGE);
+  def("FR_STAGE_SMAJOR", FR_STAGE_SMAJOR);
 #ifdef FR_TRACE_PRIO
   def("FR_TRACE_PRIO", FR_TRACE_PRIO);
 #endif

@@ -256,6 +256,9 @@ __host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? FR
 // FR_BVH_SCALAR_NODES=1: a node step whose walking lanes are all at one node reads it with
 // scalar loads (0, vector loads only: C5 trace 52.9 -> 62.3 ms, the vector memory path
 // returning 64 B per lane per step)
+#ifndef FR_STAGE_SMAJOR
+#define FR_STAGE_SMAJOR 0  // slot-major sample staging for 8-B records (A/B knob)
+#endif
 #ifndef FR_BVH_SCALAR_NODES
 #define FR_BVH_SCALAR_NODES 1
 #endif
@@ -1380,8 +1383,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         out[WPS * jj + 1] = col.y;
         if (WPS == 3) out[WPS * jj + 2] = col.z;
       } else {
-        // stage the colour; every STG-th sample of the block, and its last, go out together
-        float* sl = stage + WPS * (jj & (STG - 1u));
+        // stage the colour; every STG-th sample of the block, and its last, go out together.
+        // FR_STAGE_SMAJOR (8-B records): slot-major staging, slot j of every lane of the
+        // workgroup contiguous (a wave's writes conflict-free) instead of each lane's
+        // STG slots contiguous (lanes 8 apart on one bank)
+        constexpr bool SMAJ = FR_STAGE_SMAJOR != 0 && WPS == 2u && STG == 4u;
+        float* const stage_base = reinterpret_cast<float*>(lds);
+        auto slot_at = [&](uint32_t js) -> float* {
+          return SMAJ ? stage_base + (js * kBlock + tid) * WPS : stage + WPS * js;
+        };
+        float* sl = slot_at(jj & (STG - 1u));
         sl[0] = col.x;
         sl[1] = col.y;
         if (WPS == 3) sl[2] = col.z;
@@ -1395,7 +1406,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           const uint32_t lo = fine_item ? (jj & ~(kFineSamples - 1u)) : g0;
           float* dst = out + WPS * g0;
           if (full && kp.ks == kBlockSamples && lo == g0) {
-            if constexpr ((WPS * STG) % 4u == 0u) {
+            if constexpr (SMAJ) {
+              // two slots per 16-B store
+              const float2 a0 = *reinterpret_cast<const float2*>(slot_at(0)), a1 = *reinterpret_cast<const float2*>(slot_at(1));
+              const float2 a2 = *reinterpret_cast<const float2*>(slot_at(2)), a3 = *reinterpret_cast<const float2*>(slot_at(3));
+              reinterpret_cast<float4*>(dst)[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
+              reinterpret_cast<float4*>(dst)[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
+            } else if constexpr ((WPS * STG) % 4u == 0u) {
               // 16-B aligned: item * 192 (128) B + a multiple of 48 (32) B
               const float4* src = reinterpret_cast<const float4*>(stage);
 #pragma unroll
@@ -1413,7 +1430,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               for (uint32_t k = 0; k < WPS * STG / 2u; ++k) reinterpret_cast<float2*>(dst)[k] = src[k];
             }
           } else {
-            for (uint32_t k = WPS * (lo - g0); k < WPS * ((jj & (STG - 1u)) + 1u); ++k) dst[k] = stage[k];
+            for (uint32_t k = WPS * (lo - g0); k < WPS * ((jj & (STG - 1u)) + 1u); ++k)
+              dst[k] = SMAJ ? slot_at(k / WPS)[k % WPS] : stage[k];
           }
         }
       }
