@@ -10,7 +10,8 @@ export TMPDIR=/tmp
 for lib in "$@"; do
   name=$(basename "$lib" .so)
   for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU" \
-             "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH GRBM_GUI_ACTIVE SQ_ACTIVE_INST_SCA"; do
+             "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH GRBM_GUI_ACTIVE SQ_ACTIVE_INST_SCA" \
+             "FETCH_SIZE" "WRITE_SIZE"; do
     g=$(echo $grp | cut -c1-12 | tr ' ' _)
     out="gpurun_out/prof/$tag/$name/pmc_$g"
     mkdir -p "$out"
