@@ -699,9 +699,14 @@ def run_rank(a, plan, torch, fr):
     traffic = hbm_traffic(pmc)
     value = total_samples / elapsed / 1e6
     roof, hbm = rooflines(counts, kinds, pixels, n_prims, launches, launch_ms, traffic, issue)
-    out = base_line(a, world, value, elapsed, f"row-strips x{world}")
+    # FR_BENCH_DEVICE under the launcher puts every rank on one device (launch_plan): a
+    # rehearsal of the N-rank path, not an N-GPU measurement
+    rehearsal = world > 1 and os.environ.get("FR_BENCH_DEVICE") not in (None, "")
+    out = base_line(a, world, value, elapsed, f"row-strips x{world}"
+                    + (" (REHEARSAL: every rank on one device)" if rehearsal else ""))
     out.update({
         "launch": "single process" if world == 1 else f"torch.distributed.run, {world} ranks (one process per GPU)",
+        "rehearsal": rehearsal,
         "step": "render of the rank's strips + D2H gather of its f32 means and u8 image into pinned host memory",
         "host_sync": "each step" if a.sync_each else "after the K steps (frames streamed back to back)",
         # a frame's span, its trace's start to its sum's end: frames overlap under the frame
