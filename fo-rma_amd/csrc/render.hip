@@ -200,6 +200,39 @@ __global__ void recip_check_kernel(uint64_t base, uint64_t count, unsigned long 
   }
 }
 
+// Exhaustive check of div_rn against the correctly rounded a / b over the mantissa
+// space: the threads take every a = 1 + i 2^-23 (all 2^23 of [1, 2)), the loop every
+// b = 1 + m 2^-23 with m in [b_base, b_base + b_count), y = RN(1 / b). Division by powers
+// of two on either operand scales both results exactly while no intermediate leaves the
+// normal range, so [1, 2) x [1, 2) covers every use (rt_core.h div_rn). bad[0] counts the
+// pairs whose bits differ, first[0] holds the least (m << 23 | i) of them.
+__global__ void div_check_kernel(uint32_t b_base, uint32_t b_count, unsigned long long* bad,
+                                 unsigned long long* first) {
+  // four a per thread (i + j 2^21), so that each y = 1.0f / b serves four pairs
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (1u << 21)) return;
+  unsigned long long nbad = 0, fbad = ~0ull;
+  for (uint32_t k = 0; k < b_count; ++k) {
+    const uint32_t m = b_base + k;
+    const float b = __uint_as_float(0x3F800000u | m);
+    const float y = 1.0f / b;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t ia = i + (j << 21);
+      const float a = __uint_as_float(0x3F800000u | ia);
+      const float want = a / b, got = div_rn(a, b, y);
+      if (__float_as_uint(want) != __float_as_uint(got)) {
+        ++nbad;
+        fbad = min(fbad, (static_cast<unsigned long long>(m) << 23) | ia);
+      }
+    }
+  }
+  if (nbad) {
+    atomicAdd(bad, nbad);
+    atomicMin(first, fbad);
+  }
+}
+
 __global__ void rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, uint32_t* out) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   Rng r = rng_seed(seed, pixel, sample);
@@ -536,6 +569,9 @@ static std::string jit_defines() {
 #endif
 #ifdef FR_SKY_IEEE
   d += "#define FR_SKY_IEEE\n";
+#endif
+#ifdef FR_DIV_2STEP
+  d += "#define FR_DIV_2STEP\n";
 #endif
 #ifdef FR_NO_UNROLL_NIB
   d += "#define FR_NO_UNROLL_NIB\n";
@@ -1652,6 +1688,31 @@ int fr_selftest_recip(int device, uint64_t base, uint64_t count, uint64_t* bad, 
   HIPCHK(hipMemcpy(first, dfirst, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost));
   HIPCHK(hipFree(dbad));
   HIPCHK(hipFree(dfirst));
+  return FR_OK;
+}
+
+/* Diagnostic: div_rn against the IEEE division for every a mantissa and the b mantissas
+   [b_base, b_base + b_count) (both operands in [1, 2)); *bad = differing pairs, *first =
+   the least (b mantissa << 23 | a mantissa) among them (all ones when none). */
+int fr_selftest_div(int device, uint32_t b_base, uint32_t b_count, uint64_t* bad, uint64_t* first) {
+  if (!bad || !first || static_cast<uint64_t>(b_base) + b_count > (1ull << 23))
+    return set_error(FR_EARG, "fr_selftest_div: bad arguments");
+  SET_DEVICE(device);
+  unsigned long long* d = nullptr;
+  HIPCHK(hipMalloc(&d, 2 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(d, 0, sizeof(unsigned long long)));
+  HIPCHK(hipMemset(d + 1, 0xFF, sizeof(unsigned long long)));
+  const uint32_t chunk = 512;  // b values per launch (2^32 pairs, a few ms)
+  for (uint32_t k = 0; k < b_count; k += chunk) {
+    hipLaunchKernelGGL(div_check_kernel, dim3((1u << 21) / 256), dim3(256), 0, 0, b_base + k,
+                       min(chunk, b_count - k), d, d + 1);
+    HIPCHK(hipGetLastError());
+  }
+  unsigned long long h[2];
+  HIPCHK(hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(d));
+  *bad = h[0];
+  *first = h[1];
   return FR_OK;
 }
 

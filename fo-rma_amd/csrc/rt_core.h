@@ -276,15 +276,23 @@ __device__ __forceinline__ bool recip_nr_ok(float x) {
   return (ax >= 0x1p-126f) & (ax < 0x1p126f);
 }
 
-// a / b correctly rounded, given y = RN(1 / b): the compiler's own IEEE f32 division
-// sequence (y, q0 = a y, two FMA residual corrections) without its v_div_scale /
-// v_div_fmas / v_div_fixup steps, which are identities when a = +0 or |a| in
-// [2^-100, 2^100] and |b| in [2^-100, 2^100] (no operand or quotient near the
-// denormal / overflow range). Used only where the operand ranges hold by construction.
+// a / b correctly rounded, given y = RN(1 / b): q0 = a y and one FMA residual correction
+// q0 + (a - b q0) y (Markstein's step; the compiler's IEEE sequence takes two, as its y is
+// v_rcp_f32's 1-ulp estimate). Its v_div_scale / v_div_fmas / v_div_fixup steps are
+// identities when a = +0 or |a| in [2^-100, 2^100] and |b| in [2^-100, 2^100] (no operand,
+// quotient or residual near the denormal / overflow range), and there every operand pair
+// scales to one in [1, 2) x [1, 2) by powers of two that scale both results exactly: all
+// 2^46 such pairs are checked on the device (fr_selftest_div,
+// tests/test_gpu_parity.py::test_div_rn_exhaustive). Used only where the operand ranges
+// hold by construction. FR_DIV_2STEP: the second correction as well (the round-4 form).
 __device__ __forceinline__ float div_rn(float a, float b, float y) {
   const float q0 = a * y;
   const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
+#ifdef FR_DIV_2STEP
   return __builtin_fmaf(__builtin_fmaf(-b, q1, a), y, q1);
+#else
+  return q1;
+#endif
 }
 #endif
 

@@ -90,6 +90,7 @@ EXPORTS = (
     "fr_ctx_trace_log_read", "fr_mctx_create", "fr_mctx_free", "fr_mctx_count", "fr_mctx_ctx", "fr_mctx_render",
     "fr_mctx_sync", "fr_mctx_frame", "fr_mctx_download",
     "fr_render_hip", "fr_render_hip_multi", "fr_selftest_ops", "fr_selftest_rng", "fr_selftest_recip",
+    "fr_selftest_div",
     "fr_post_process", "fr_post_process_device", "fr_rgb_to_rgba_device", "fr_ctx_jit_info", "fr_selftest_jit",
     "fr_ctx_prepare", "fr_ctx_jit_state", "fr_jit_wait",
 )
@@ -175,6 +176,8 @@ def lib():
         L.fr_rgb_to_rgba_device.argtypes = [vp, vp, vp, C.c_size_t]
     if hasattr(L, "fr_selftest_recip"):  # absent from A/B builds of older sources
         L.fr_selftest_recip.argtypes = [C.c_int, C.c_uint64, C.c_uint64, P(C.c_uint64), P(C.c_uint32)]
+    if hasattr(L, "fr_selftest_div"):  # absent from A/B builds of older sources
+        L.fr_selftest_div.argtypes = [C.c_int, C.c_uint32, C.c_uint32, P(C.c_uint64), P(C.c_uint64)]
     if hasattr(L, "fr_ctx_jit_info"):  # absent from A/B builds of older sources
         L.fr_ctx_jit_info.argtypes = [vp, P(C.c_int), P(C.c_double), P(C.c_int)]
         L.fr_ctx_prepare.argtypes = [vp, vp, P(FrCamera), P(FrParams)]

@@ -320,6 +320,10 @@ int fr_selftest_rng(int device, uint64_t seed, uint32_t pixel, uint32_t sample, 
    1.0f / x for every f32 bit pattern in [base, base + count): mismatches per exponent
    field in bad[256], first mismatching pattern in first[256] (0xFFFFFFFF = none). */
 int fr_selftest_recip(int device, uint64_t base, uint64_t count, uint64_t* bad, uint32_t* first);
+/* Compare div_rn (q0 = a y, one FMA residual correction, y = RN(1 / b)) with the IEEE
+   division for every a in [1, 2) and the b = 1 + m 2^-23, m in [b_base, b_base + b_count):
+   *bad = differing pairs, *first = least (m << 23 | a's mantissa) among them (~0 = none). */
+int fr_selftest_div(int device, uint32_t b_base, uint32_t b_count, uint64_t* bad, uint64_t* first);
 /* No device needed: hiprtc compiles the scene-specialised kernel for `arch` with n 64-B
    device records (16 u32 each, kind in word 15); targs = trace_kernel's 8 template
    arguments, or NULL for the headline's (all boxes, diffuse, depth <= 8, 8-B records);

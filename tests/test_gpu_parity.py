@@ -80,6 +80,17 @@ def test_recip_nr_exhaustive(gpu):
     assert not bad[1:253].any(), {e: (int(bad[e]), hex(int(first[e]))) for e in np.nonzero(bad[1:253])[0] + 1}
 
 
+def test_div_rn_exhaustive(gpu):
+    """div_rn (q0 = a y, one FMA residual correction, y = RN(1 / b)) equals the IEEE
+    division for all 2^46 operand pairs in [1, 2) x [1, 2), the mantissa space every
+    in-range use (jitter, sky parameter, sphere roots) scales to exactly."""
+    import ctypes as C
+    bad = C.c_uint64(0)
+    first = C.c_uint64(0)
+    gpu.check(gpu.lib().fr_selftest_div(0, 0, 1 << 23, C.byref(bad), C.byref(first)))
+    assert bad.value == 0, (bad.value, hex(first.value >> 23), hex(first.value & 0x7FFFFF))
+
+
 def test_device_max3_and_min3_match_fmaxf_fminf(gpu):
     """The slab test's v_max3_f32 (tn) and v_min3_f32 (tf) against the host's fmaxf/fminf
     chains, bit for bit, on edge values (NaN, +-0, +-inf, denormals). Slab distances come
