@@ -881,8 +881,10 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   KParams kp;
   kp.W = p->width;
   kp.H = p->height;
-  kp.rW = 1.0f / static_cast<float>(p->width);
-  kp.rH = 1.0f / static_cast<float>(p->height);
+  kp.rW = 1.0f / (static_cast<float>(p->width) * 16777216.0f);  // = RN(1 / W) 2^-24
+  kp.rH = 1.0f / (static_cast<float>(p->height) * 16777216.0f);
+  kp.sW = static_cast<float>(p->width) * 16777216.0f;
+  kp.sH = static_cast<float>(p->height) * 16777216.0f;
   kp.spp = p->spp;
   kp.max_depth = p->max_depth;
   kp.seed = p->seed;

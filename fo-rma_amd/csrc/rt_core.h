@@ -126,6 +126,8 @@ FR_HD uint32_t rng_next(Rng& r) {  // xoshiro128+ 1.0
 FR_HD float rng_f32(Rng& r) {
   return static_cast<float>((rng_next(r) ^ 0x80000000u) >> 8) * 5.9604644775390625e-08f;
 }
+// 2^24 rng_f32(r): the integer before the scale, as an f32 (exact)
+FR_HD float rng_f32_scaled(Rng& r) { return static_cast<float>((rng_next(r) ^ 0x80000000u) >> 8); }
 
 // 2*r - 1 for that r: (k - 2^23) * 2^-23 is exact in f32 and equals the arithmetic
 // shift (int32)u >> 8 scaled by 2^-23, so shift + convert + scale replace the
@@ -548,12 +550,12 @@ FR_HD V3 sky(V3 d) { return sky_from_t(sky_t(d)); }
 // v_sqrt_f32 and the compiler's two FMA residual corrections without the denormal
 // scaling and class fix-up (identities for dd in [2^-96, 2^126]); and d.y / len by
 // div_rn(d.y, len, recip_nr(len)) (recip_nr exact for len's exponent range there, div_rn's
-// steps identities for |d.y| in {0} u [2^-100, 2^100]; a quotient below 2^-26, where the
-// core sequence could differ in the denormal range, gives 1 + q = 1 either way). Other
-// lanes take the plain expression. Bit-identical to sky_t: fr_selftest_ops op 14.
+// steps identities for |d.y| in {0} u [2^-100, 2^63], and |d.y| <= len <= 2^63). A d.y
+// below 2^-100 in magnitude needs no guard of its own: with len >= 2^-48 both sequences
+// give |q| < 2^-50 (the core one's residual may be denormal there), and 1 + q = 1 either
+// way. Other lanes take the plain expression. Bit-identical to sky_t: fr_selftest_ops op 14.
 __device__ __forceinline__ float sky_t_fast_from(float dy, float dd) {
-  const float ay = __builtin_fabsf(dy);
-  const bool fast = (dd >= 0x1p-96f) & (dd <= 0x1p126f) & ((ay >= 0x1p-100f) | (ay == 0.0f));
+  const bool fast = (dd >= 0x1p-96f) & (dd <= 0x1p126f);
   if (fast) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const float s = __builtin_amdgcn_sqrtf(dd);

@@ -156,7 +156,10 @@ struct KParams {
   uint32_t b0, nb;    // this pass renders sample blocks [b0, b0 + nb)
   uint32_t n_items;   // nb x P work items (pixel slot, block); < 2^32 per pass
   uint32_t tiles_magic, tiles_shift;  // x / n_tiles = fastdiv(x, tiles_magic, tiles_shift)
-  float rW, rH;                       // RN(1 / W), RN(1 / H) (host IEEE division)
+  // the jitter's (x + r) / W as 2^24 (x + r) / (2^24 W), the 2^24 folded into the operands
+  // (exact scalings): rW = RN(1 / W) 2^-24 = RN(1 / (2^24 W)) (host IEEE division), sW =
+  // 2^24 W; the same for H
+  float rW, rH, sW, sH;
   uint32_t row_magic, row_shift;      // x / tiles_per_row = fastdiv(x, row_magic, row_shift)
   uint32_t band_h;                    // FR_FLAG_MT_BANDS: rows per band, H / 4 (tracer.rs:87)
   uint32_t ks;          // sample slots per work item in the sample buffer: min(spp, kBlockSamples)
@@ -342,11 +345,18 @@ enum { SC_ITER, SC_CLAIM, SC_JIT, SC_NEED, SC_REJ, SC_CAM, SC_SCAT, SC_HIT, SC_S
 // the last written t is tracked separately from the winner's.
 // (two 32-bit popcounts: a 64-bit one leaves a 64-bit count whose compare the SALU
 // cannot do, and the compiler moved it to the VALU)
-__device__ __forceinline__ uint32_t lanes_set(bool b) {
-  const unsigned long long m = __builtin_amdgcn_ballot_w64(b);
+// This lane's bit of a lane mask as its branch condition: LLVM's inverse ballot, which
+// becomes the mask itself (an s_and_saveexec on it, no VALU). Declared by its intrinsic
+// name: the hiprtc that builds the scene kernel (the one PyTorch ships) predates clang's
+// __builtin_amdgcn_inverse_ballot_w64, its LLVM has the intrinsic.
+extern "C" __device__ bool fr_inverse_ballot(unsigned long long) __asm("llvm.amdgcn.inverse.ballot.i64");
+__device__ __forceinline__ bool lane_in(unsigned long long m) { return fr_inverse_ballot(m); }
+
+__device__ __forceinline__ uint32_t lanes_in(unsigned long long m) {
   return static_cast<uint32_t>(__builtin_popcount(static_cast<uint32_t>(m)) +
                                __builtin_popcount(static_cast<uint32_t>(m >> 32)));
 }
+__device__ __forceinline__ uint32_t lanes_set(bool b) { return lanes_in(__builtin_amdgcn_ballot_w64(b)); }
 
 // Per-lane select on a lane mask (a ballot): one v_cndmask_b32. The compiler turned chains
 // of selects on compare results into branches with the conditions materialised as 0/1
@@ -573,8 +583,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   __syncthreads();
 
 
-  const float fW = static_cast<float>(kp.W), fH = static_cast<float>(kp.H);
-
   enum : uint32_t { NEED_NONE = 0, NEED_LENS = 1, NEED_SPHERE = 2 };
   uint32_t depth = 0;  // scatters of the path (not NIB: wnib holds them)
   // NIB: the winners as 4-bit entries, the last one pushed in bits 28..31 and the first in
@@ -768,8 +776,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           diag_seg0 = nseg;
 #endif
           s_end = min(s + (fine ? kFineSamples : kBlockSamples), kp.spp);
-          fx = static_cast<float>(x);
-          fy = static_cast<float>(yrow);
+          fx = static_cast<float>(x) * 16777216.0f;  // 2^24 x, exact (x, yrow < 2^24)
+          fy = static_cast<float>(yrow) * 16777216.0f;
           need_jit = true;
           need_item = false;
         }
@@ -780,10 +788,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       // a sample starts: jitter (tracer.rs:171-172), then its lens sample in step 1. One
       // place for the first sample of a block and the next sample of the same block, so
       // the wave runs it once per iteration
-      const float r0 = rng_f32(rng);
-      const float r1 = rng_f32(rng);
-      d.x = div_rn(fx + r0, fW, kp.rW);  // (fx + r0) / fW, numerator +0 or in [2^-24, 2^32]
-      d.y = div_rn(fy + r1, fH, kp.rH);
+      // 2^24 (x + r) = RN(2^24 x + 2^24 r) (rounding commutes with the exact scaling), so
+      // the quotients are (x + r) / W's bits: numerator +0 or in [1, 2^56], divisor 2^24 W
+      const float r0 = rng_f32_scaled(rng);
+      const float r1 = rng_f32_scaled(rng);
+      d.x = div_rn(fx + r0, kp.sW, kp.rW);
+      d.y = div_rn(fy + r1, kp.sH, kp.rH);
       if (MT) d.y = d.y + vofs;  // render_mt's band offset (tracer.rs:103)
       need = NEED_LENS;
       need_jit = false;
@@ -796,25 +806,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     if (need != NEED_NONE) {
       SEC(SC_NEED);
       // 1. merged rejection loop
-      // dd >= 2^46: the lane still rejects (the loop test and the next pass's branch are
-      // one compare on it; a bool carried through the loop cost a select and a compare per
-      // pass to ballot)
+      // mrej: the lanes that still reject (dd >= 2^46), one compare per pass: the loop test
+      // counts it and the next pass's branch and the accept test take it back as their
+      // lane condition (inverse ballot, no instruction; a compare on dd in each of them
+      // cost the pass a second v_cmp, a bool carried through the loop a select and a compare)
       float px = 0.0f, py = 0.0f, pz = 0.0f, dd = kUnitBallScaled;
       const bool sph = need == NEED_SPHERE;
+      unsigned long long mrej = __builtin_amdgcn_read_exec();  // every lane here starts with a try
       do {
         SEC(SC_REJ);
         DIAG_WAVE(DG_LENS_W);
         DIAG_LANE(DG_LENS_L);
-        if (dd >= kUnitBallScaled) {
+        if (lane_in(mrej)) {
           // the test in the 2^23-scaled domain (rng_signed_unit_scaled): same decisions
           px = rng_signed_unit_scaled(rng);
           py = rng_signed_unit_scaled(rng);
           if (sph) pz = rng_signed_unit_scaled(rng);  // a circle try keeps pz = 0
           dd = px * px + py * py + pz * pz;
         }
-      } while (lanes_set(dd >= kUnitBallScaled) > static_cast<uint32_t>(KREJ));
+        mrej = __builtin_amdgcn_ballot_w64(dd >= kUnitBallScaled);
+      } while (lanes_in(mrej) > static_cast<uint32_t>(KREJ));
       SEC(SC_ACC);
-      if (dd < kUnitBallScaled) {
+      if (!lane_in(mrej)) {
         px *= kSignedUnitScale;  // the accepted point, 2r - 1 per coordinate (exact)
         py *= kSignedUnitScale;
         pz *= kSignedUnitScale;

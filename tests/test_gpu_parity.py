@@ -161,8 +161,8 @@ def test_fast_sky_parameter_is_bit_identical(gpu):
     """sky_t_fast (the sky blend parameter with guarded core sqrt/division sequences, the
     trace kernel's default; FR_SKY_IEEE builds the plain one) against the plain correctly
     rounded sky_t on the device, bit for bit (op 14 returns the XOR of both results' bits),
-    over random directions of every scale and the guards' edges: tiny, zero, -0, denormal
-    and huge components."""
+    over random directions of every scale, the guards' edges (tiny, zero, -0, denormal
+    and huge components) and tiny d.y beside x, z in the fast range."""
     import ctypes as C
     rng = np.random.default_rng(14)
     fp = C.POINTER(C.c_float)
@@ -172,7 +172,13 @@ def test_fast_sky_parameter_is_bit_identical(gpu):
     edges = np.array([0.0, -0.0, 1e-45, -1e-45, 2.0 ** -100, -(2.0 ** -100), 2.0 ** -101, 2.0 ** -60, 2.0 ** -48,
                       2.0 ** -47, 2.0 ** 62, 2.0 ** 63, 2.0 ** 64, 1.0, -1.0, 3e-39, 1e-30], dtype=np.float32)
     e = np.array(np.meshgrid(edges, edges, edges)).reshape(3, -1)
-    v = np.concatenate([v, e, e[[1, 2, 0]]], axis=1).astype(np.float32)
+    # d.y below 2^-100 (normal and denormal) beside x and z that put dot(d, d) in the fast
+    # range: the case with no guard of its own
+    m = 100000
+    tiny = (rng.choice([-1.0, 1.0], m) * 2.0 ** rng.uniform(-149, -100, m)).astype(np.float32)
+    big = (rng.standard_normal((2, m)) * 2.0 ** rng.uniform(-47, 62, (2, m))).astype(np.float32)
+    t = np.stack([big[0], tiny, big[1]])
+    v = np.concatenate([v, e, e[[1, 2, 0]], t], axis=1).astype(np.float32)
     x, y = np.ascontiguousarray(v[0]), np.ascontiguousarray(v[1])  # z of lane i is y[i + 1] (op 14)
     out = np.empty_like(x)
     gpu.check(gpu.lib().fr_selftest_ops(0, 14, x.ctypes.data_as(fp), y.ctypes.data_as(fp), x.size,
