@@ -620,7 +620,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #endif
   float* out = kw.samples;   // the item's first sample slot (item-major buffer)
   Rng rng{0u, 0u, 0u, 0u};
-  bool active = true, need_item = true, need_jit = false, have_ray = false;
+  // (a lane needs a work item when its block's samples are done: s == s_end, both 0 at the
+  // start, and a claim that finds no pixel leaves them equal; a compare the loop's ballot
+  // takes directly, where a carried bool cost a select and a compare per iteration)
+  bool active = true, need_jit = false, have_ray = false;
   uint32_t need = NEED_NONE;
 
 #ifdef FR_PROF
@@ -666,13 +669,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       g_fr_iter_times[(gw >> 6) * 1024u + diag_iter] = __builtin_amdgcn_s_memrealtime();
     ++diag_iter;
 #endif
-    const unsigned long long m = __ballot(need_item);
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(s == s_end);  // lanes needing an item
     // Lanes whose item is done wait (idle) until FR_CLAIM_MIN of them need one, or until no
     // active lane has other work: the claim step (its lane permutes and item setup) then
     // runs for several lanes at once instead of in nearly every iteration for one or two.
     // Only when work starts changes, never what a sample computes (results bit-identical).
     constexpr uint32_t CLAIM_MIN = NIB ? FR_CLAIM_MIN_NIB : FR_CLAIM_MIN;
-    if (m && (CLAIM_MIN <= 1 || lanes_set(need_item) >= CLAIM_MIN || m == __ballot(1))) {
+    if (m && (CLAIM_MIN <= 1 || lanes_in(m) >= CLAIM_MIN || m == __ballot(1))) {
       SEC(SC_CLAIM);
       // 0. claim work items: the free lanes take consecutive items of the wave's batch;
       // when it runs out, the first free lane reserves the next batch of kBatch = 64
@@ -736,7 +739,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       }
       q_next = grab ? base + (n - avail) : next + n;
       const uint32_t item = r < avail ? next + r : base + (r - avail);
-      if (need_item && item >= kp.n_items) {
+      if (lane_in(m) && item >= kp.n_items) {
 #ifdef FR_DIAG
         if (gw < 65536) {
           const unsigned long long now = __builtin_amdgcn_s_memrealtime();
@@ -749,7 +752,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         active = false;  // queue drained
         continue;
       }
-      if (need_item) {
+      if (lane_in(m)) {
         SEC(SC_SETUP);
         const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
         bool ok = xy != 0xFFFFFFFFu;
@@ -779,7 +782,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           fx = static_cast<float>(x) * 16777216.0f;  // 2^24 x, exact (x, yrow < 2^24)
           fy = static_cast<float>(yrow) * 16777216.0f;
           need_jit = true;
-          need_item = false;
         }
       }
     }
@@ -809,29 +811,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       // mrej: the lanes that still reject (dd >= 2^46), one compare per pass: the loop test
       // counts it and the next pass's branch and the accept test take it back as their
       // lane condition (inverse ballot, no instruction; a compare on dd in each of them
-      // cost the pass a second v_cmp, a bool carried through the loop a select and a compare)
-      float px = 0.0f, py = 0.0f, pz = 0.0f, dd = kUnitBallScaled;
-      const bool sph = need == NEED_SPHERE;
-      unsigned long long mrej = __builtin_amdgcn_read_exec();  // every lane here starts with a try
-      do {
+      // cost the pass a second v_cmp, a bool carried through the loop a select and a compare).
+      // Every lane here makes the first try, outside the loop: px, py and dd need no
+      // initial values then
+      // (the sphere/circle condition as a lane mask: one compare serves the tries and the
+      // camera/scatter branch, which the compiler otherwise tested with a second v_cmp)
+      const unsigned long long msph = __builtin_amdgcn_ballot_w64(need == NEED_SPHERE);
+      float pz = 0.0f;  // a circle try keeps pz = 0
+      DIAG_WAVE(DG_LENS_W);
+      DIAG_LANE(DG_LENS_L);
+      // the test in the 2^23-scaled domain (rng_signed_unit_scaled): same decisions
+      float px = rng_signed_unit_scaled(rng);
+      float py = rng_signed_unit_scaled(rng);
+      if (lane_in(msph)) pz = rng_signed_unit_scaled(rng);
+      float dd = px * px + py * py + pz * pz;
+      unsigned long long mrej = __builtin_amdgcn_ballot_w64(dd >= kUnitBallScaled);
+      while (lanes_in(mrej) > static_cast<uint32_t>(KREJ)) {
         SEC(SC_REJ);
         DIAG_WAVE(DG_LENS_W);
         DIAG_LANE(DG_LENS_L);
         if (lane_in(mrej)) {
-          // the test in the 2^23-scaled domain (rng_signed_unit_scaled): same decisions
           px = rng_signed_unit_scaled(rng);
           py = rng_signed_unit_scaled(rng);
-          if (sph) pz = rng_signed_unit_scaled(rng);  // a circle try keeps pz = 0
+          if (lane_in(msph)) pz = rng_signed_unit_scaled(rng);
           dd = px * px + py * py + pz * pz;
         }
         mrej = __builtin_amdgcn_ballot_w64(dd >= kUnitBallScaled);
-      } while (lanes_in(mrej) > static_cast<uint32_t>(KREJ));
+      }
       SEC(SC_ACC);
       if (!lane_in(mrej)) {
         px *= kSignedUnitScale;  // the accepted point, 2r - 1 per coordinate (exact)
         py *= kSignedUnitScale;
         pz *= kSignedUnitScale;
-        if (!sph) {
+        if (!lane_in(msph)) {
           SEC(SC_CAM);
           // Camera::get_ray (camera.rs:62-72)
 #if !defined(FR_CAM_RESIDENT) && defined(__HIP_DEVICE_COMPILE__)
@@ -1451,10 +1463,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #ifdef FR_DIAG
       if (s + 1u == s_end && diag_tb < (1u << 20)) atomicAdd(&g_fr_tb_cost[diag_tb], nseg - diag_seg0);
 #endif
-      if (++s == s_end)
-        need_item = true;
-      else
-        need_jit = true;  // next sample of the block, same stream
+      if (++s != s_end) need_jit = true;  // next sample of the block, same stream (else: a new item)
     }
     PROF_MARK(PF_END);
     SEC(SC_LATCH);
