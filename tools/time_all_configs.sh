@@ -1,5 +1,6 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+export FR_SCENE_JIT="${FR_SCENE_JIT:-1}"  # the scene-specialised kernel, as the bench runs it
 T="timeout -k 10 120 python3 tools/time_config.py"
 : > gpurun_out/configs.jsonl
 $T scene_01 256 256 4 4 5 >> gpurun_out/configs.jsonl &&
