@@ -1,6 +1,7 @@
 // Host BVH build: full-sweep SAH (every centroid position on all three axes) with
 // leaves of at most kBvhLeafMax primitives, object-median splits where the depth cap
-// (kBvhStack) would otherwise be at risk, nodes holding both children's boxes.
+// (kBvhStack) would otherwise be at risk, nodes holding both children's boxes. O(n log n):
+// the three axis orders are sorted once and kept sorted per node by stable partitions.
 #include "bvh.h"
 
 #include <math.h>
@@ -85,64 +86,92 @@ uint32_t balanced_levels(uint32_t n, uint32_t leaf_max) {
   return l;
 }
 
+// The builder keeps, per axis, the items' ids sorted by (centroid on that axis, list index)
+// within every open node's range. A node's three SAH sweeps then read their orders without
+// sorting, and a split stable-partitions the other two axes' ids by side, so each level costs
+// O(n) (the round-5 builder sorted every node's items four times: 1.06 s for 150k spheres,
+// 39.5 ms for C5; this one builds the same trees, checked by digest in
+// tests/test_host_sanitizers.py). A leaf's slots list its items in the order of the axis
+// its parent split on (list order for a root leaf).
 struct Builder {
-  std::vector<Item>& items;
+  const std::vector<Item>& items;  // by item id
   std::vector<BvhNode>& nodes;
+  std::vector<uint32_t>& slots;    // item id per leaf slot, relative to slot 0 of this tree
   float pad;
   uint32_t leaf_max;
   uint32_t slot_base;  // leaf slots are absolute positions in the shared order array
+  std::vector<uint32_t> idx[3];
+  std::vector<uint8_t> on_left;  // by item id, scratch of one split
+  std::vector<uint32_t> tmp;
+  std::vector<double> right;
 
-  Box3 bounds(uint32_t begin, uint32_t end, Box3* cbox) const {
+  Builder(const std::vector<Item>& it, std::vector<BvhNode>& nd, std::vector<uint32_t>& sl, float p, uint32_t lm,
+          uint32_t base)
+      : items(it), nodes(nd), slots(sl), pad(p), leaf_max(lm), slot_base(base) {
+    const uint32_t n = static_cast<uint32_t>(items.size());
+    for (int k = 0; k < 3; ++k) {
+      idx[k].resize(n);
+      for (uint32_t i = 0; i < n; ++i) idx[k][i] = i;
+      std::sort(idx[k].begin(), idx[k].end(), [&](uint32_t x, uint32_t y) {
+        return items[x].c[k] < items[y].c[k] || (items[x].c[k] == items[y].c[k] && items[x].index < items[y].index);
+      });
+    }
+    on_left.assign(n, 0);
+    tmp.resize(n);
+    right.resize(n + 1);
+    slots.assign(n, 0);
+  }
+
+  Box3 bounds(const uint32_t* ids, uint32_t n, Box3* cbox) const {
     Box3 box;
-    for (uint32_t i = begin; i < end; ++i) {
-      box.grow(items[i].box);
-      if (cbox) cbox->grow(items[i].c);
+    for (uint32_t i = 0; i < n; ++i) {
+      box.grow(items[ids[i]].box);
+      if (cbox) cbox->grow(items[ids[i]].c);
     }
     return box;
   }
 
-  // Reference to the subtree over items[begin, end) at depth `depth`.
-  uint32_t build(uint32_t begin, uint32_t end, uint32_t depth) {
+  // Reference to the subtree over range [begin, end) at depth `depth`; `pa` is the axis the
+  // parent split on (-1 at the root: list order).
+  uint32_t build(uint32_t begin, uint32_t end, uint32_t depth, int pa) {
     const uint32_t n = end - begin;
-    // FR_BVH_CT = c (A/B): SAH termination with a node step costing c primitive tests: a node
-    // of at most FR_BVH_LEAF_CAP (8) primitives becomes a leaf when testing them all costs no
-    // more than the best split (c + the children's area-weighted counts); off: every node
-    // of at most leaf_max primitives is a leaf and every larger one is split
-    static const double ct = [] {
-      const char* e = getenv("FR_BVH_CT");
-      return e ? atof(e) : -1.0;
-    }();
-    static const uint32_t leaf_cap = [] {
-      const char* e = getenv("FR_BVH_LEAF_CAP");
-      const int v = e ? atoi(e) : 8;
-      return static_cast<uint32_t>(v >= 1 && v <= static_cast<int>(kBvhLeafCountMax) ? v : 8);
-    }();
-    if (ct < 0.0 && n <= leaf_max) return bvh_leaf_ref(slot_base + begin, n);
-    Box3 cbox;
-    const Box3 box = bounds(begin, end, &cbox);
-    if (ct >= 0.0 && n <= std::max(leaf_cap, leaf_max)) {
-      if (n == 1) return bvh_leaf_ref(slot_base + begin, n);
-      double best = INFINITY;
-      for (int k = 0; k < 3; ++k) {
-        if (!(cbox.hi[k] - cbox.lo[k] > 0.0f)) continue;
-        double c = INFINITY;
-        sweep_split(begin, end, k, &c);
-        best = std::min(best, c);
+    if (n <= leaf_max) {
+      if (pa < 0) {  // a root leaf keeps list order (ids are list-ordered)
+        for (uint32_t i = 0; i < n; ++i) slots[begin + i] = begin + i;
+      } else {
+        for (uint32_t i = 0; i < n; ++i) slots[begin + i] = idx[pa][begin + i];
       }
-      const double a = box.area();
-      if (!(a > 0.0) || a * n <= ct * a + best) return bvh_leaf_ref(slot_base + begin, n);
+      return bvh_leaf_ref(slot_base + begin, n);
     }
+    Box3 cbox;
+    (void)bounds(idx[0].data() + begin, n, &cbox);
     // SAH while the subtree can still be finished below the cap by balanced splits
     // (a median split at depth d with d + levels(n) = kBvhStack leaves the deepest
     // internal node at kBvhStack - 1)
+    int axis = -1;
     uint32_t mid = begin;
-    if (depth + balanced_levels(n, leaf_max) < kBvhStack) mid = sah_split(begin, end, box, cbox);
-    if (mid == begin || mid == end) mid = median_split(begin, end, cbox);
+    if (depth + balanced_levels(n, leaf_max) < kBvhStack) sah_split(begin, end, cbox, &axis, &mid);
+    if (mid == begin || mid == end) median_split(begin, end, cbox, &axis, &mid);
+    // ids of the left side first on every axis, each side in its axis order
+    for (uint32_t i = begin; i < end; ++i) on_left[idx[axis][i]] = i < mid;
+    for (int k = 0; k < 3; ++k) {
+      if (k == axis) continue;
+      uint32_t l = begin, r = 0;
+      for (uint32_t i = begin; i < end; ++i) {
+        const uint32_t id = idx[k][i];
+        if (on_left[id])
+          idx[k][l++] = id;
+        else
+          tmp[r++] = id;
+      }
+      std::copy(tmp.begin(), tmp.begin() + r, idx[k].begin() + l);
+    }
     const uint32_t at = static_cast<uint32_t>(nodes.size());
     nodes.push_back(BvhNode{});
-    const Box3 l = bounds(begin, mid, nullptr), r = bounds(mid, end, nullptr);
-    const uint32_t rl = build(begin, mid, depth + 1);
-    const uint32_t rr = build(mid, end, depth + 1);
+    const Box3 l = bounds(idx[axis].data() + begin, mid - begin, nullptr);
+    const Box3 r = bounds(idx[axis].data() + mid, end - mid, nullptr);
+    const uint32_t rl = build(begin, mid, depth + 1, axis);
+    const uint32_t rr = build(mid, end, depth + 1, axis);
     BvhNode& nd = nodes[at];
     // conservative padding
     for (int k = 0; k < 3; ++k) {
@@ -160,9 +189,7 @@ struct Builder {
     return at;
   }
 
-  // Object median on the longest centroid axis; halves by index when the centroids
-  // coincide.
-  uint32_t median_split(uint32_t begin, uint32_t end, const Box3& cbox) {
+  static int longest(const Box3& cbox, float* ext_out) {
     int axis = 0;
     float ext = -1.0f;
     for (int k = 0; k < 3; ++k)
@@ -170,123 +197,63 @@ struct Builder {
         ext = cbox.hi[k] - cbox.lo[k];
         axis = k;
       }
-    const uint32_t mid = begin + (end - begin) / 2;
-    if (ext > 0.0f)
-      std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end,
-                       [&](const Item& x, const Item& y) { return x.c[axis] < y.c[axis]; });
-    return mid;
+    *ext_out = ext;
+    return axis;
   }
 
-  // SAH split: on each axis the centroids sorted and the area x count cost evaluated at every
-  // position; the cheapest of the three axes. C5 trace 45.6 ms, against 46.5 for the sweep on
-  // the longest axis only (FR_BVH_AXES=1) and 51.3 for 12 bins on the longest axis (8 bins
-  // 48.5, 16 bins 52.3: binned trees walked at very different speeds). FR_BVH_BINS=k (A/B):
-  // k bins on the longest axis instead (0: object medians).
-  uint32_t sah_split(uint32_t begin, uint32_t end, const Box3& box, const Box3& cbox) {
-    (void)box;
-    int axis = 0;
-    float ext = -1.0f;
-    for (int k = 0; k < 3; ++k)
-      if (cbox.hi[k] - cbox.lo[k] > ext) {
-        ext = cbox.hi[k] - cbox.lo[k];
-        axis = k;
+  // Object median on the longest centroid axis (ties by list index); halves in list order
+  // when the centroids coincide (every axis order is then list order).
+  void median_split(uint32_t begin, uint32_t end, const Box3& cbox, int* axis, uint32_t* mid) {
+    float ext;
+    const int a = longest(cbox, &ext);
+    *axis = ext > 0.0f ? a : 0;
+    *mid = begin + (end - begin) / 2;
+  }
+
+  // SAH split: on each axis the cost (area x count per side) at every position of the
+  // centroid order; the cheapest of the three axes (the first on ties), at its first
+  // cheapest position. C5 trace 45.6 ms, against 46.5 for the sweep on the longest axis only
+  // and 51.3 for 12 bins on the longest axis (8 bins 48.5, 16 bins 52.3: binned trees walked
+  // at very different speeds; profiles/AB_LOG.md).
+  void sah_split(uint32_t begin, uint32_t end, const Box3& cbox, int* axis, uint32_t* mid) {
+    float ext;
+    (void)longest(cbox, &ext);
+    if (!(ext > 0.0f)) return;
+    double best = INFINITY;
+    for (int k = 0; k < 3; ++k) {
+      if (!(cbox.hi[k] - cbox.lo[k] > 0.0f)) continue;
+      double cost = INFINITY;
+      const uint32_t i = sweep(begin, end, k, &cost);
+      if (cost < best && i) {
+        best = cost;
+        *axis = k;
+        *mid = begin + i;
       }
-    if (!(ext > 0.0f)) return begin;
-    static const int B = [] {
-      const char* e = getenv("FR_BVH_BINS");
-      const int v = e ? atoi(e) : -1;
-      return v >= 0 && v <= 64 ? v : -1;
-    }();
-    static const bool all_axes = [] {
-      const char* e = getenv("FR_BVH_AXES");
-      return !(e && atoi(e) == 1);
-    }();
-    if (B < 0) {
-      if (!all_axes) return sweep_split(begin, end, axis, nullptr);
-      double best = INFINITY;
-      int best_axis = -1;
-      for (int k = 0; k < 3; ++k) {
-        if (!(cbox.hi[k] - cbox.lo[k] > 0.0f)) continue;
-        double cost = INFINITY;
-        sweep_split(begin, end, k, &cost);
-        if (cost < best) {
-          best = cost;
-          best_axis = k;
-        }
-      }
-      return best_axis < 0 ? begin : sweep_split(begin, end, best_axis, nullptr);
     }
-    if (B < 2) return begin;
-    return binned_split(begin, end, cbox, axis, ext, B);
   }
 
-  // items[begin, end) sorted by centroid on `axis` (ties by list index: deterministic);
-  // returns the least-cost partition point (begin if none), its cost in *cost_out if given
-  uint32_t sweep_split(uint32_t begin, uint32_t end, int axis, double* cost_out) {
-    std::sort(items.begin() + begin, items.begin() + end, [&](const Item& x, const Item& y) {
-      return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.index < y.index);
-    });
+  // the least-cost partition position of the range in axis k's order (0 if none)
+  uint32_t sweep(uint32_t begin, uint32_t end, int k, double* cost_out) {
     const uint32_t n = end - begin;
-    std::vector<double> right(n + 1, 0.0);
+    const uint32_t* ids = idx[k].data() + begin;
     Box3 acc;
     for (uint32_t i = n; i > 0; --i) {
-      acc.grow(items[begin + i - 1].box);
+      acc.grow(items[ids[i - 1]].box);
       right[i - 1] = acc.area();
     }
     Box3 lacc;
     double best = INFINITY;
     uint32_t best_i = 0;
     for (uint32_t i = 1; i < n; ++i) {
-      lacc.grow(items[begin + i - 1].box);
+      lacc.grow(items[ids[i - 1]].box);
       const double cost = lacc.area() * i + right[i] * (n - i);
       if (cost < best) {
         best = cost;
         best_i = i;
       }
     }
-    if (cost_out) *cost_out = best;
-    return best_i ? begin + best_i : begin;
-  }
-
-  uint32_t binned_split(uint32_t begin, uint32_t end, const Box3& cbox, int axis, float ext, int B) {
-    Box3 bb[64];
-    uint32_t bc[64] = {};
-    const float lo = cbox.lo[axis], scale = B / ext;
-    auto bin_of = [&](const Item& it) {
-      int b = static_cast<int>((it.c[axis] - lo) * scale);
-      return b < 0 ? 0 : (b >= B ? B - 1 : b);
-    };
-    for (uint32_t i = begin; i < end; ++i) {
-      const int b = bin_of(items[i]);
-      bb[b].grow(items[i].box);
-      ++bc[b];
-    }
-    double left_area[64], best = INFINITY;
-    uint32_t left_count[64];
-    Box3 acc;
-    uint32_t cnt = 0;
-    for (int b = 0; b < B; ++b) {
-      acc.grow(bb[b]);
-      cnt += bc[b];
-      left_area[b] = acc.area();
-      left_count[b] = cnt;
-    }
-    Box3 racc;
-    uint32_t rcnt = 0;
-    int best_b = -1;
-    for (int b = B - 1; b > 0; --b) {
-      racc.grow(bb[b]);
-      rcnt += bc[b];
-      const double cost = left_area[b - 1] * left_count[b - 1] + racc.area() * rcnt;
-      if (left_count[b - 1] && rcnt && cost < best) {
-        best = cost;
-        best_b = b;
-      }
-    }
-    if (best_b < 0) return begin;
-    auto it = std::partition(items.begin() + begin, items.begin() + end,
-                             [&](const Item& x) { return bin_of(x) < best_b; });
-    return static_cast<uint32_t>(it - items.begin());
+    *cost_out = best;
+    return best_i;
   }
 };
 
@@ -329,9 +296,10 @@ bool build_range(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end
   if (balanced_levels(n, leaf_max) >= kBvhStack) return false;
   if (order.size() + n + kBvhLeafCountMax >= (1u << kBvhSlotBits)) return false;
   if (nodes.size() + n >= kBvhLeaf) return false;
-  Builder b{items, nodes, pad, leaf_max, static_cast<uint32_t>(order.size())};
-  root = b.build(0, n, 0);
-  for (const Item& it : items) order.push_back(it.index);
+  std::vector<uint32_t> slots;
+  Builder b(items, nodes, slots, pad, leaf_max, static_cast<uint32_t>(order.size()));
+  root = b.build(0, n, 0, -1);
+  for (uint32_t id : slots) order.push_back(items[id].index);
   return true;
 }
 

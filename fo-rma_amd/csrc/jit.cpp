@@ -19,8 +19,8 @@
 //      check, or fails to load, is deleted and the kernel compiled again once;
 //   3. hiprtc: on the caller's thread when it waits (fr_ctx_prepare, FR_FLAG_SCENE_JIT_WAIT),
 //      else on one background worker thread while renders run the compiled-in kernel.
-// Bounds: at most kMaxModules loaded modules (least recently used unloaded first, after its
-// device drains), kMaxCode code objects in memory and kMaxDiskFiles files on disk.
+// Bounds: at most kMaxModules loaded modules (least recently used unloaded first, after
+// every stream it was launched on has passed its last launch), kMaxCode code objects in memory and kMaxDiskFiles files on disk.
 #include <dirent.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
@@ -51,6 +51,17 @@ namespace fr {
 namespace {
 
 constexpr size_t kMaxModules = 64;    // loaded (device, key) modules per process
+constexpr size_t kMaxStreamEvents = 32;  // per module: completed entries are pruned beyond this
+
+// FR_JIT_MAX_MODULES (tests only): a smaller module bound, so a test can force evictions
+size_t max_modules() {
+  static const size_t n = [] {
+    const char* e = getenv("FR_JIT_MAX_MODULES");
+    const long v = e && *e ? atol(e) : 0;
+    return v > 0 ? static_cast<size_t>(v) : kMaxModules;
+  }();
+  return n;
+}
 constexpr size_t kMaxCode = 128;      // code objects held in memory per process
 constexpr size_t kMaxDiskFiles = 256; // .hsaco files kept in the disk cache
 
@@ -239,12 +250,17 @@ struct CodeEntry {
   uint64_t used = 0;
 };
 
-// A module's last launch: jit_note_launch records it (an event on the launch's stream); an
-// evicted module is unloaded after that event, not after a drain of the whole device.
-// (The event is destroyed when its module is unloaded, never at process exit: the runtime
-// may be gone by then.)
+// A module's launches still in flight: jit_note_launch records, per stream the module was
+// launched on, an event after the launch (streams are in order, so one event per stream
+// covers every earlier launch there). An evicted module is unloaded after all of them, not
+// after a drain of the whole device. One context launches on two streams (multi-pass renders
+// and overlapping frames alternate) and contexts on one device share a module, so a single
+// "last launch" event would miss the other stream's launch. Guarded by `mu`: renders on
+// several threads note launches of one module concurrently. (The events are destroyed when
+// the module is unloaded, never at process exit: the runtime may be gone by then.)
 struct ModuleUse {
-  hipEvent_t last = nullptr;
+  std::mutex mu;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> last;  // (stream, event after its last launch)
 };
 
 struct Module {
@@ -364,18 +380,21 @@ const std::string& toolchain() {
   return t;
 }
 
-// Unload a module evicted from the table once its last launch has finished: a launch of it
-// may still be queued on a stream (its event, jit_note_launch). No caller holds it
-// (unpinned): a render that looked it up holds its pin from the lookup through the launch
+// Unload a module evicted from the table once every launch of it has finished: launches
+// may still be queued on any stream it was launched on (jit_note_launch). No caller holds
+// it (unpinned): a render that looked it up holds its pin from the lookup through the launch
 // and the event record, so no launch of it can follow.
 void unload_evicted(const Module& m) {
   int cur = -1;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(m.device);
-  if (m.pin->last) {
-    (void)hipEventSynchronize(m.pin->last);
-    (void)hipEventDestroy(m.pin->last);
-    m.pin->last = nullptr;
+  {
+    std::lock_guard<std::mutex> g(m.pin->mu);
+    for (auto& se : m.pin->last) {
+      (void)hipEventSynchronize(se.second);
+      (void)hipEventDestroy(se.second);
+    }
+    m.pin->last.clear();
   }
   (void)hipModuleUnload(m.mod);
   if (cur >= 0) (void)hipSetDevice(cur);
@@ -404,11 +423,28 @@ int jit_wait_all() {
 void jit_note_launch(const std::shared_ptr<void>& pin, hipStream_t stream) {
   ModuleUse* u = static_cast<ModuleUse*>(pin.get());
   if (!u) return;
-  if (!u->last && hipEventCreateWithFlags(&u->last, hipEventDisableTiming) != hipSuccess) {
-    u->last = nullptr;
-    return;
+  std::lock_guard<std::mutex> g(u->mu);
+  for (auto& se : u->last)
+    if (se.first == stream) {
+      (void)hipEventRecord(se.second, stream);
+      return;
+    }
+  // a stream not seen before (a new context, or a stream handle reused after one closed):
+  // first drop entries whose launches have finished, so the list stays short
+  if (u->last.size() >= kMaxStreamEvents) {
+    auto keep = u->last.begin();
+    for (auto& se : u->last) {
+      if (hipEventQuery(se.second) == hipSuccess)
+        (void)hipEventDestroy(se.second);
+      else
+        *keep++ = se;
+    }
+    u->last.erase(keep, u->last.end());
   }
-  (void)hipEventRecord(u->last, stream);
+  hipEvent_t ev = nullptr;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+  (void)hipEventRecord(ev, stream);
+  u->last.emplace_back(stream, ev);
 }
 
 int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* out, JitStats* stats,
@@ -536,7 +572,7 @@ int jit_trace_kernel(int device, const JitSpec& spec, bool wait, hipFunction_t* 
     // evict the least recently used modules beyond the bound, among those no caller pins
     // (a pin is copied only under this lock, so an unpinned module stays unpinned here)
     std::vector<Module> evicted;
-    while (R.modules.size() > kMaxModules) {
+    while (R.modules.size() > max_modules()) {
       auto victim = R.modules.end();
       for (auto v = R.modules.begin(); v != R.modules.end(); ++v)
         if (v->second.pin.use_count() == 1 && (victim == R.modules.end() || v->second.used < victim->second.used))

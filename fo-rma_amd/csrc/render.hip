@@ -418,6 +418,8 @@ void release_device_copies(fr_scene* s) {
 
 using namespace fr;
 
+constexpr int kCntWords = 64;  // counter words per frame slot (fr_ctx::d_cnt)
+
 struct fr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -438,7 +440,8 @@ struct fr_ctx {
   int occupancy = 0;  // trace-kernel workgroups per CU of the last launch (occupancy API)
   float* d_mean = nullptr;
   uint8_t* d_u8 = nullptr;
-  // [0..3] counters, [4..] diagnostics; [31] queue head: one set of 32 per frame slot
+  // [0..3] counters, [4..30] and [32..63] diagnostics (FR_SECCNT, FR_PROF, FR_DIAG builds);
+  // [31] queue head: one set of kCntWords per frame slot
   unsigned long long* d_cnt = nullptr;
   unsigned long long* last_cnt = nullptr;  // the last render's set
   // Frame pipeline (FR_FRAME_PIPE): one-pass frames alternate between two
@@ -645,7 +648,7 @@ static int launch_persistent(const Grid& g, size_t lds, hipStream_t st, KArgs a,
     size_t bytes = sizeof(KArgs);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
     HIPCHK(hipModuleLaunchKernel(jfn, blocks, 1, 1, kBlock, 1, 1, static_cast<uint32_t>(lds), st, nullptr, cfg));
-    jit_note_launch(jr->pin, st);  // an LRU eviction of the module waits for this launch only
+    jit_note_launch(jr->pin, st);  // an LRU eviction waits for the last launch on every stream used
   } else {
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, st, a);
   }
@@ -768,7 +771,7 @@ int fr_ctx_create(int device, void* stream, fr_ctx** out) {
       hipEventCreateWithFlags(&c->ev_fslot[1], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fslot[2], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fslot[3], hipEventDisableTiming) != hipSuccess ||
-      hipMalloc(&c->d_cnt, fr_ctx::kFrameSlots * 32 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&c->d_cnt, fr_ctx::kFrameSlots * kCntWords * sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&c->d_wcnt, fr_ctx::kFrameSlots * 3 * sizeof(unsigned long long) * kMaxWgPerCu * (kBlock / 64u) *
                                 c->num_cus) !=
           hipSuccess) {  // one set per pass slot (traces of consecutive passes overlap)
@@ -979,7 +982,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   const bool relayout = !fpipe || nfs != c->fs_n || slot_bytes != c->fs_bytes;
   if (relayout) c->frame_slot = 0;
   const int fs = fpipe ? c->frame_slot % nfs : 0;
-  unsigned long long* cnt = c->d_cnt + 32 * fs;
+  unsigned long long* cnt = c->d_cnt + kCntWords * fs;
   const int slots = passes > 1 ? 2 : fpipe ? nfs : 1;
   if (kp.P && nb_pass && slot_bytes * slots > c->cap_samples) {
     if (c->d_samples) HIPCHK(hipFree(c->d_samples));
@@ -1089,7 +1092,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     if (c->fslot_used[k] && (k == fs || relayout)) HIPCHK(hipStreamWaitEvent(setup, c->ev_fslot[k], 0));
   c->fs_n = nfs;
   c->fs_bytes = slot_bytes;
-  HIPCHK(hipMemsetAsync(cnt, 0, 32 * sizeof(unsigned long long), setup));
+  HIPCHK(hipMemsetAsync(cnt, 0, kCntWords * sizeof(unsigned long long), setup));
 #ifdef FR_DIAG
   {
     const unsigned long long z[2] = {0, 0};
@@ -1207,7 +1210,7 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
   if (!c->pending) return set_error(FR_EARG, "fr_ctx_sync: nothing rendered");
   HIPCHK(hipEventSynchronize(c->ev1));  // the frame's end (on the sum stream when pipelined)
   if (st) {
-    unsigned long long cnt[32] = {};
+    unsigned long long cnt[kCntWords] = {};
     HIPCHK(hipMemcpy(cnt, c->last_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
 #ifdef FR_PROF
     {
@@ -1220,6 +1223,8 @@ int fr_ctx_sync(fr_ctx* c, fr_stats* st) {
 #ifdef FR_SECCNT
     fprintf(stderr, "FR_SECCNT [");
     for (int k = 0; k < SC_N; ++k) fprintf(stderr, k ? ", %llu" : "%llu", cnt[4 + k]);
+    fprintf(stderr, "]\nFR_SECLANES [");
+    for (int k = 0; k < SC_N; ++k) fprintf(stderr, k ? ", %llu" : "%llu", cnt[32 + k]);
     fprintf(stderr, "]\n");
 #endif
 #ifdef FR_DIAG

@@ -326,16 +326,23 @@ enum { PF_CLAIM, PF_REJ, PF_HIT, PF_SHADE, PF_END, PF_N };
 // The first SC_N regions are counted; the others only mark a boundary in the listing, and
 // their entries follow from a counted one (SETUP ~ CLAIM, ACC = NEED, POSTHIT = HIT,
 // POSTSHADE = LATCH = ITER; GRAB = the batches the queue hands out).
+// The BVH walk's node step and leaf tests each have a scalar path (every walking lane at one
+// node or leaf) and a vector path, exclusive per entry: they are separate regions (SC_NODES /
+// SC_NODEV, SC_LTESTS / SC_LTESTV), so a static count never adds both paths' instructions to
+// one entry. FR_SECCNT also sums the active lanes of every entry (counters[32 + k]).
 enum { SC_ITER, SC_CLAIM, SC_JIT, SC_NEED, SC_REJ, SC_CAM, SC_SCAT, SC_HIT, SC_SKY, SC_SHADE, SC_END, SC_NODE,
-       SC_LEAF, SC_LTEST, SC_N, SC_GRAB = SC_N, SC_SETUP, SC_ACC, SC_POSTHIT, SC_POSTSHADE, SC_LATCH };
+       SC_LEAF, SC_NODES, SC_NODEV, SC_LTESTS, SC_LTESTV, SC_N, SC_GRAB = SC_N, SC_SETUP, SC_ACC, SC_POSTHIT,
+       SC_POSTSHADE, SC_LATCH };
 #if defined(FR_SEC_MARKS) && defined(__HIP_DEVICE_COMPILE__)
 #define SEC(k) asm volatile(";FRSEC " #k)
 #elif defined(FR_SECCNT)
 #define SEC(k)                                                                       \
   do {                                                                               \
     const unsigned long long m_ = __ballot(1);                                       \
-    if ((k) < SC_N && lane == static_cast<uint32_t>(__ffsll(m_) - 1))              \
+    if ((k) < SC_N && lane == static_cast<uint32_t>(__ffsll(m_) - 1)) {            \
       atomicAdd(&sec_cnt[(k) < SC_N ? (k) : 0], 1u);                               \
+      atomicAdd(&sec_cnt[SC_N + ((k) < SC_N ? (k) : 0)], lanes_in(m_));            \
+    }                                                                                \
   } while (0)
 #else
 #define SEC(k) do {} while (0)
@@ -577,8 +584,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   }
 #endif
 #ifdef FR_SECCNT
-  __shared__ uint32_t sec_cnt[SC_N];
-  if (tid < SC_N) sec_cnt[tid] = 0;
+  __shared__ uint32_t sec_cnt[2 * SC_N];  // wave entries, then active lanes summed over them
+  if (tid < 2 * SC_N) sec_cnt[tid] = 0;
 #endif
   __syncthreads();
 
@@ -1013,6 +1020,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                 // rays of one tile): scalar loads, the slab arithmetic on SGPR operands (the
                 // distinct asm ends keep the two paths from being merged over copies of the
                 // node into VGPRs)
+                SEC(SC_NODES);
                 const RecRef nd = rec_at(sc.bvh, ref0);
                 const float4 r = nd[3];
                 node_step(nd[0], nd[1], nd[2], __float_as_uint(r.x), __float_as_uint(r.y));
@@ -1020,6 +1028,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               } else
 #endif
               {
+                SEC(SC_NODEV);
                 const uint32_t nb0 = ref * 64u;  // node byte offset (< 2^32: nodes < 2^26)
                 const uint4 nr = __builtin_bit_cast(uint4, buf_load4(sc.bvh, nb0 + 48u));
                 node_step(buf_load4(sc.bvh, nb0), buf_load4(sc.bvh, nb0 + 16u), buf_load4(sc.bvh, nb0 + 32u), nr.x, nr.y);
@@ -1071,7 +1080,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               const uint32_t first0 = leaf0 & ((1u << kBvhSlotBits) - 1u);
               const uint32_t cnt0 = ((leaf0 >> kBvhSlotBits) & 15u) + 1u;
               for (uint32_t kk = 0; kk < cnt0; ++kk) {
-                SEC(SC_LTEST);
+                SEC(SC_LTESTS);
                 leaf_test(ord[first0 + kk], rec_at(sc.lrec, first0 + kk));
               }
               asm volatile("; bvh leaf: scalar");
@@ -1079,7 +1088,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #endif
             {
               for (uint32_t kk = 0; kk < cnt; ++kk) {
-                SEC(SC_LTEST);
+                SEC(SC_LTESTV);
                 const uint32_t slot = first + kk;
                 // buffer loads: 32-bit offsets from the arrays' bases (slots < 2^26)
                 struct LeafRec {
@@ -1487,6 +1496,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #ifdef FR_SECCNT
   __syncthreads();
   if (tid < SC_N) atomicAdd(&kw.counters[4 + tid], static_cast<unsigned long long>(sec_cnt[tid]));
+  if (tid < SC_N) atomicAdd(&kw.counters[32 + tid], static_cast<unsigned long long>(sec_cnt[SC_N + tid]));
 #endif
 #ifdef FR_PROF
   if (lane == 0)

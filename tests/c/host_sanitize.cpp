@@ -22,6 +22,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -55,10 +56,23 @@ static void bvh_report(const std::vector<fr_prim>& prims, bool force) {
   std::vector<fr::BvhNode> nodes;
   std::vector<uint32_t> order;
   float extent = 0.0f;
+  const auto t0 = std::chrono::steady_clock::now();
   const bool ok = fr::build_segments(prims, segs, nodes, order, force, &extent);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   const uint32_t depth = ok ? fr::bvh_max_depth(segs, nodes) : 0u;
-  printf(", \"bvh%s\": {\"ok\": %d, \"segments\": %zu, \"nodes\": %zu, \"order\": %zu, \"depth\": %u}",
-         force ? "_forced" : "", ok ? 1 : 0, segs.size(), nodes.size(), order.size(), depth);
+  // a digest of the tree (node boxes, references, leaf order): builder changes that must
+  // not change the tree are checked with it
+  uint64_t h = 0xcbf29ce484222325ull;
+  auto mix = [&h](const void* p, size_t n) {
+    for (size_t i = 0; i < n; ++i) h = (h ^ static_cast<const unsigned char*>(p)[i]) * 0x100000001b3ull;
+  };
+  if (!nodes.empty()) mix(nodes.data(), nodes.size() * sizeof(fr::BvhNode));
+  if (!order.empty()) mix(order.data(), order.size() * sizeof(uint32_t));
+  if (!segs.empty()) mix(segs.data(), segs.size() * sizeof(fr::BvhSegment));
+  printf(", \"bvh%s\": {\"ok\": %d, \"segments\": %zu, \"nodes\": %zu, \"order\": %zu, \"depth\": %u, "
+         "\"build_ms\": %.3f, \"digest\": \"%016llx\"}",
+         force ? "_forced" : "", ok ? 1 : 0, segs.size(), nodes.size(), order.size(), depth, ms,
+         static_cast<unsigned long long>(h));
 }
 
 static int do_json(const char* path) {

@@ -108,6 +108,26 @@ def test_generator_scene_bvh_build_clean(exe, tmp_path):
     # the full-sweep SAH tree (bvh.cpp): internal nodes below the stack's 16 levels (the
     # launch sizes its LDS stack to depth + 1 levels), leaves of at most 4 spheres
     assert r["bvh"]["depth"] < 16 and 10000 / 4 - 1 <= r["bvh"]["nodes"] < 10000
+    # the tree the C5 timings were taken on (round 5's sort-per-node builder built the same
+    # bytes: nodes, leaf order, segments); a builder change that moves it shows here
+    assert r["bvh"]["digest"] == "74bc9267b6b5e9e6", r["bvh"]
+
+
+# forced trees of the bundled scenes (fnv-1a over nodes, leaf order and segments), equal for
+# round 5's builder (sorting every node's items per axis) and round 6's (presorted orders)
+BUNDLED_TREE_DIGESTS = {
+    "scene_01": "db0be86289f89f8d", "scene_02": "9402547a91b47399", "scene_03": "346a873c38c9159b",
+    "scene_04": "51895897d1998ae2", "scene_05": "8ee866288e39c8d0", "scene_06": "191d4432c7c74f33",
+    "scene_08": "3a4d7944ad02b602", "scene_09": "6f417d5af3a20a2f",
+}
+
+
+def test_bvh_trees_of_bundled_scenes_are_pinned(exe):
+    res = _run(exe, "json", *[p for p in SCENES if os.path.basename(p)[:8] in BUNDLED_TREE_DIGESTS])
+    assert len(res) == len(BUNDLED_TREE_DIGESTS)
+    for r in res:
+        name = os.path.basename(r["file"])[:8]
+        assert r["bvh_forced"]["digest"] == BUNDLED_TREE_DIGESTS[name], (name, r["bvh_forced"])
 
 
 def test_degenerate_bvh_inputs_build_clean(exe, tmp_path):

@@ -382,3 +382,54 @@ def test_one_shot_save_image_never_queues_a_compile(gpu, tmp_path):
             assert not list(cache.iterdir()), "a cold one-shot save_image queued a compile"
     assert res["warm"]["state"] == gpu.FR_JIT_USED, res
     assert res["cold"]["sha"] == res["warm"]["sha"], res
+
+
+_EVICT = r'''
+import hashlib, json, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "fo-rma_amd"))
+import forma_rt as fr
+W, H = 1920, 1080
+x = fr.Scene.from_file(fr.scene_path("scene_01"), W, H)
+y = fr.Scene.from_file(fr.scene_path("scene_08"), 96, 64)
+z = fr.Scene.builtin(0, 96, 64)
+px = fr.make_params(W, H, 256, 8, scene_jit="wait")
+py, pz = (fr.make_params(96, 64, 8, 8, scene_jit="wait", seed=s) for s in (3, 4))
+# every code object compiled once (the module bound is 1, so these loads evict each other)
+for sc, p in ((x, fr.make_params(32, 16, 1, 8, scene_jit="wait")), (y, py), (z, pz)):
+    c = fr.RenderContext(0); c.render(sc, sc.camera, p); c.sync(); c.close()
+a, b = fr.RenderContext(0), fr.RenderContext(0)
+a.render(x, x.camera, px)          # ~13 passes, alternating two trace streams; no host wait
+a.render(y, y.camera, py)          # A's pin moves to y's module: x's is unpinned, still in flight
+b.render(z, z.camera, pz)          # loading z's module evicts x's while its passes run
+out = {}
+for name, c, w, h in (("y", a, 96, 64), ("z", b, 96, 64)):
+    st = c.sync(); m, u = c.download(w, h)
+    out[name] = {"sha": hashlib.sha256(m.tobytes()).hexdigest(), "used": c.jit_info()["used"], "seg": st["segments"]}
+    c.close()
+print(json.dumps(out))
+'''
+
+
+@pytest.mark.gpu
+def test_module_eviction_waits_for_every_stream(gpu):
+    """ADVICE r5: an evicted scene-kernel module is unloaded only after the last launch on
+    every stream it was launched on. With the module bound forced to 1 (FR_JIT_MAX_MODULES),
+    a 13-pass frame (traces alternating between the context's two streams) is still running
+    when its module is unpinned and then evicted by another context's load; the process must
+    finish without a fault, and the frames rendered around the eviction must equal the
+    compiled-in kernel's."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FR_JIT_MAX_MODULES="1", FR_SAMPLE_BUFFER_GB="0.5")
+    env.pop("FR_SCENE_JIT", None)
+    out = subprocess.run([sys.executable, "-c", _EVICT, root], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    import hashlib
+    for name, sc, seed in (("y", gpu.Scene.from_file(gpu.scene_path("scene_08"), 96, 64), 3),
+                           ("z", gpu.Scene.builtin(0, 96, 64), 4)):
+        m, u, st = gpu.render(sc, sc.camera, 96, 64, 8, 8, seed=seed)
+        assert r[name]["used"], r
+        assert r[name]["sha"] == hashlib.sha256(m.tobytes()).hexdigest() and r[name]["seg"] == st["segments"], r

@@ -26,8 +26,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "fo-rma_amd", "csrc")
 # counted regions, in trace_kernel.h's SC_* order
+# (the BVH walk's scalar and vector paths are separate regions: SC_NODES / SC_NODEV after the
+# node step's common head SC_NODE, SC_LTESTS / SC_LTESTV for one leaf test)
 REGIONS = ["SC_ITER", "SC_CLAIM", "SC_JIT", "SC_NEED", "SC_REJ", "SC_CAM", "SC_SCAT", "SC_HIT", "SC_SKY", "SC_SHADE",
-           "SC_END", "SC_NODE", "SC_LEAF", "SC_LTEST"]
+           "SC_END", "SC_NODE", "SC_LEAF", "SC_NODES", "SC_NODEV", "SC_LTESTS", "SC_LTESTV"]
 # marker-only regions: the counted region whose entries they share
 DERIVED = {"SC_SETUP": "SC_CLAIM", "SC_ACC": "SC_NEED", "SC_POSTHIT": "SC_HIT", "SC_POSTSHADE": "SC_ITER",
            "SC_LATCH": "SC_ITER"}
@@ -170,23 +172,29 @@ def combine(static_path, seccnt_path, segments, valu_measured, grabs=0):
     st = json.load(open(static_path))
     line = [ln for ln in open(seccnt_path) if "FR_SECCNT" in ln][-1]
     counts = json.loads(line.split("FR_SECCNT", 1)[1])
+    lanes_l = [ln for ln in open(seccnt_path) if "FR_SECLANES" in ln]
+    lanes = json.loads(lanes_l[-1].split("FR_SECLANES", 1)[1]) if lanes_l else [0] * len(counts)
     tab = st["regions"]
     rows, tot = [], 0.0
     for name in REGIONS + list(DERIVED) + ["SC_GRAB"]:
         v = tab.get(name, {}).get("valu", 0)
         if name in REGIONS:
-            n = counts[REGIONS.index(name)]
+            n, ln = counts[REGIONS.index(name)], lanes[REGIONS.index(name)]
         elif name in DERIVED:
-            n = counts[REGIONS.index(DERIVED[name])]
+            n, ln = counts[REGIONS.index(DERIVED[name])], lanes[REGIONS.index(DERIVED[name])]
         else:
-            n = grabs
-        rows.append((name, v, n, v * n))
+            n, ln = grabs, 0
+        rows.append((name, v, n, v * n, ln))
         tot += v * n
     out = {"regions": [], "total_valu_model": tot, "valu_measured": valu_measured,
            "model_over_measured": tot / valu_measured if valu_measured else None, "segments": segments}
-    for name, v, n, vn in rows:
+    for name, v, n, vn, ln in rows:
+        # active lanes per entry, and the region's idle lane-slots: VALU x (64 - active lanes)
+        act = ln / n if n and ln else None
         out["regions"].append({"region": name, "static_valu": v, "wave_entries": n, "valu": vn,
-                               "share": vn / tot if tot else 0.0, "lane_slots_per_segment": vn * 64.0 / segments})
+                               "share": vn / tot if tot else 0.0, "lane_slots_per_segment": vn * 64.0 / segments,
+                               "active_lanes_per_entry": round(act, 2) if act else None,
+                               "idle_lane_slots": v * (64.0 * n - ln) if ln else None})
     return out
 
 

@@ -2,6 +2,9 @@
 kernel-trace statistics.
 
     python tools/pmc_summary.py gpurun_out/prof/<tag> [--write profiles/pmc_trace_kernel.json]
+    python tools/pmc_summary.py --runs DIR... [--segments N]   (one rocprofv3 --pmc run per DIR,
+        each with --kernel-trace --stats: counters averaged over the trace_kernel launches, the
+        launch time from the runs' warm launches, VALU lane-slots per segment when N is given)
 
 --write stores the per-launch HBM bytes that bench.py reports as roofline.traffic."""
 import collections
@@ -28,7 +31,47 @@ def load(dirpath):
     return res
 
 
+def runs_summary(dirs, segments=None):
+    out = collections.defaultdict(list)
+    warm_ns = []
+    for dpath in dirs:
+        for f in glob.glob(os.path.join(dpath, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if "trace_kernel" in r["Kernel_Name"]:
+                    out[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for f in glob.glob(os.path.join(dpath, "**", "*kernel_trace.csv"), recursive=True):
+            ts = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(f))
+                        if "trace_kernel" in r["Kernel_Name"])
+            warm_ns += [e - s for s, e in ts[1:]]  # the first (cold) launch of each run set aside
+    res = {k: sum(v) / len(v) for k, v in out.items()}
+    res["launches_per_counter"] = {k: len(v) for k, v in out.items()}
+    ns = sum(warm_ns) / len(warm_ns) if warm_ns else None
+    res["warm_launch_ns_under_counters"] = ns
+    if ns and "SQ_INSTS_VALU" in res and "GRBM_GUI_ACTIVE" in res:
+        clk = res["GRBM_GUI_ACTIVE"] / 8 / (ns * 1e-9)
+        res["clock_ghz"] = clk / 1e9
+        res["valu_issue_frac"] = res["SQ_INSTS_VALU"] / (ns * 1e-9) / (1024 * clk / 2)
+    if "SQ_WAIT_ANY" in res and "SQ_WAVE_CYCLES" in res:
+        res["wait_any_over_wave_cycles"] = res["SQ_WAIT_ANY"] / res["SQ_WAVE_CYCLES"]
+    if "WRITE_SIZE" in res:
+        res["write_bytes"] = res["WRITE_SIZE"] * 1024
+    if "FETCH_SIZE" in res:
+        res["fetch_bytes_x2"] = 2 * res["FETCH_SIZE"] * 1024
+    if segments and "SQ_INSTS_VALU" in res:
+        res["segments"] = segments
+        res["valu_lane_slots_per_segment"] = res["SQ_INSTS_VALU"] * 64 / segments
+    return res
+
+
 def main():
+    if sys.argv[1] == "--runs":
+        args = sys.argv[2:]
+        seg = None
+        if "--segments" in args:
+            seg = float(args[args.index("--segments") + 1])
+            args = args[:args.index("--segments")] + args[args.index("--segments") + 2:]
+        print(json.dumps(runs_summary(args, seg), indent=1))
+        return
     d = load(sys.argv[1])
     hbm = None
     ns = d.get("avg_ns", 0)
