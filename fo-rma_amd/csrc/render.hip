@@ -88,6 +88,12 @@ struct DeviceCopy {
   uint32_t bvh_levels = kBvhStack;
   bool att_nonneg = true;  // every attenuation component finite and >= +0 (no -0)
   bool diffuse = true;     // no metal or dielectric scatter class (trace_kernel MAT = 1)
+  // attenuation classes: the scene's distinct attenuations (bit patterns), when there are at
+  // most kNibbleMaxPrims of them (else 0): BVH kernels with 8-B records store a path's
+  // winners as classes (KScene::acls), and sum_nib_kernel reads this table instead of one
+  // entry per primitive
+  uint32_t n_aclass = 0;
+  size_t off_acls = 0, off_acls_att = 0;
   std::vector<uint32_t> rec_words;  // the n 64-B records as uploaded (the scene-specialised build's constants)
 };
 
@@ -307,7 +313,13 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   c->n_runs = static_cast<uint32_t>(runs.size() / 4);
   c->off_runs = off;
   off = align_up(off + (runs.size() ? runs.size() : 4) * 4, 256);
+  c->off_acls = off;
+  off = align_up(off + m * 4, 256);
+  c->off_acls_att = off;
+  off = align_up(off + (kNibbleMaxPrims + 1) * 16, 256);
   std::vector<unsigned char> host(off, 0);
+  std::vector<float4> aclass;  // distinct attenuations, first appearance order
+  bool aclass_ok = true;
   bool nonneg = true;
   bool diffuse = true;
   if (!bvh_nodes.empty()) memcpy(&host[c->off_bvh], bvh_nodes.data(), bvh_nodes.size() * sizeof(BvhNode));
@@ -361,6 +373,18 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
     memcpy(&host[c->off_mat + 16 * i], &mat, 16);
     memcpy(&host[c->off_cls + 4 * i], &cls, 4);
     memcpy(&host[c->off_att + 16 * i], &att, 16);
+    {
+      uint32_t k = 0;
+      while (k < aclass.size() && memcmp(&aclass[k], &att, 12) != 0) ++k;
+      if (k == aclass.size()) {
+        if (aclass.size() < kNibbleMaxPrims)
+          aclass.push_back(att);
+        else
+          aclass_ok = false;
+      }
+      const uint32_t kc = k < kNibbleMaxPrims ? k : 0u;
+      memcpy(&host[c->off_acls + 4 * i], &kc, 4);
+    }
     for (float a : {att.x, att.y, att.z})
       if (!(a >= 0.0f) || std::signbit(a) || !std::isfinite(a)) nonneg = false;
     memcpy(&g[3].w, &kind, 4);  // kind bits in g3.w
@@ -370,6 +394,11 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
   if (n) memcpy(c->rec_words.data(), &host[c->off_rec], 64u * static_cast<size_t>(n));
   c->att_nonneg = nonneg;
   c->diffuse = diffuse;
+  c->n_aclass = aclass_ok && n ? static_cast<uint32_t>(aclass.size()) : 0u;
+  for (uint32_t k = 0; k <= kNibbleMaxPrims; ++k) {  // entries past the classes: the unit attenuation
+    const float4 a = k < aclass.size() ? aclass[k] : make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    memcpy(&host[c->off_acls_att + 16 * k], &a, 16);
+  }
   // the BVH leaves' records, in leaf-slot order
   for (size_t slot = 0; slot < bvh_order.size(); ++slot)
     memcpy(&host[c->off_lrec + 64 * slot], &host[c->off_rec + 64 * static_cast<size_t>(bvh_order[slot])], 64);
@@ -579,6 +608,9 @@ static std::string jit_defines() {
 #ifdef FR_NO_UNROLL_NIB
   d += "#define FR_NO_UNROLL_NIB\n";
 #endif
+#if FR_BOX_FMA
+  def("FR_BOX_FMA", FR_BOX_FMA);
+#endif
 #ifdef FR_PROF
   d += "#define FR_PROF\n";  // section clocks go to the launch's counters, not device globals
 #endif
@@ -657,6 +689,11 @@ static int launch_persistent(const Grid& g, size_t lds, hipStream_t st, KArgs a,
 
 template <int KS, bool HP, bool BV, bool MT = false>
 static int launch_depth(bool small_depth, const Grid& g, size_t lds, hipStream_t st, const KArgs& a, JitReq* jr) {
+  if constexpr (BV && !MT) {
+    // diffuse scenes of <= 15 distinct attenuations: 8-B records of attenuation classes
+    if ((a.kp.flags & KF_DEFER) && (a.kp.flags & KF_NIBBLE) && (a.kp.flags & KF_DIFFUSE))
+      return launch_persistent<KS, HP, FR_KREJ_BVH, kSmallDepth, true, false, 2, 1>(g, lds, st, a, jr);
+  }
   if constexpr (!BV && !MT) {
     if (a.kp.flags & KF_DEFER) {
       if ((a.kp.flags & KF_NIBBLE) && (a.kp.flags & KF_DIFFUSE))
@@ -853,6 +890,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   ks.mat = reinterpret_cast<const float4*>(b + dc->off_mat);
   ks.cls = reinterpret_cast<const uint32_t*>(b + dc->off_cls);
   ks.att = reinterpret_cast<const float4*>(b + dc->off_att);
+  ks.acls = reinterpret_cast<const uint32_t*>(b + dc->off_acls);
   ks.n = dc->n;
   // FR_BVH=0 forces the in-order loop (A/B and tests)
   const char* bvh_env = getenv("FR_BVH");
@@ -916,14 +954,20 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   // the deferred unwind (kDeferMaxPrims); FR_DEFER=0 keeps the unwind in the trace kernel,
   // FR_DEFER=1 the 12-B records for small scenes too (A/B)
   const char* defer_env = getenv("FR_DEFER");
-  const bool defer = small_depth && dc->n <= kDeferMaxPrims && !use_bvh && !(p->flags & FR_FLAG_MT_BANDS) &&
-                     !(defer_env && strcmp(defer_env, "0") == 0);
-  const bool nibble = defer && dc->n <= kNibbleMaxPrims && !(defer_env && strcmp(defer_env, "1") == 0);
-  if (defer) kp.flags |= KF_DEFER;
-  if (nibble) kp.flags |= KF_NIBBLE;
   // FR_MAT=0 keeps the general shading step for diffuse-only scenes (A/B, tests)
   const char* mat_env = getenv("FR_MAT");
-  if (dc->diffuse && !(mat_env && strcmp(mat_env, "0") == 0)) kp.flags |= KF_DIFFUSE;
+  const bool diffuse_k = dc->diffuse && !(mat_env && strcmp(mat_env, "0") == 0);
+  // BVH kernels defer too when the scene is diffuse and has at most 15 distinct attenuations
+  // (C5: one): 8-B records of attenuation classes
+  const bool bvh_nib = use_bvh && small_depth && diffuse_k && dc->n_aclass > 0 &&
+                       !(p->flags & FR_FLAG_MT_BANDS) && !(defer_env && strcmp(defer_env, "0") == 0);
+  const bool defer = bvh_nib || (small_depth && dc->n <= kDeferMaxPrims && !use_bvh &&
+                                 !(p->flags & FR_FLAG_MT_BANDS) && !(defer_env && strcmp(defer_env, "0") == 0));
+  const bool nibble =
+      bvh_nib || (defer && dc->n <= kNibbleMaxPrims && !(defer_env && strcmp(defer_env, "1") == 0));
+  if (defer) kp.flags |= KF_DEFER;
+  if (nibble) kp.flags |= KF_NIBBLE;
+  if (diffuse_k) kp.flags |= KF_DIFFUSE;
   const uint32_t wps = nibble && !kSkyDefer ? 2u : 3u;  // words per sample in the buffer
   const size_t per_block = static_cast<size_t>(kp.P) * kp.ks * wps * sizeof(float);
   uint32_t want_passes = 1;
@@ -1016,8 +1060,9 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
                                          : static_cast<size_t>(p->max_depth ? p->max_depth : 1u) * kBlock *
                                                sizeof(uint32_t);
   const size_t n_rec = dc->n <= kRecLds ? dc->n : 0u;
-  const size_t stage_n = stage_samples(use_bvh);
-  const size_t lds = (stage_n > 1 && !use_bvh ? kBlock * stage_n * wps * sizeof(float) : 0u) + (n_att ? n_att + 1 : 0) * 16 +
+  const size_t stage_n = stage_samples(use_bvh, nibble);
+  const size_t lds = (stage_n > 1 && (!use_bvh || nibble) ? kBlock * stage_n * wps * sizeof(float) : 0u) +
+                     (n_att ? n_att + 1 : 0) * 16 +
                      n_rec * 64 + stack_bytes + (use_bvh ? dc->bvh_levels * kBlock * sizeof(uint32_t) : 0u);
   // the scene-specialised kernel (jit.h): list-loop scenes of <= kJitMaxPrims primitives,
   // when the caller asks (FR_FLAG_SCENE_JIT; FR_SCENE_JIT=1 / 0 forces it on / off)
@@ -1135,7 +1180,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       // persistent grid: the resident workgroup count (launch_persistent)
       uint32_t blocks = 0;
       Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy, &blocks,
-                use_bvh && stage_n > 1 && !FR_BVH_RSTAGE ? kBlock * stage_n * 3 * sizeof(float) : 0u};
+                use_bvh && !nibble && stage_n > 1 && !FR_BVH_RSTAGE ? kBlock * stage_n * 3 * sizeof(float) : 0u};
       // pipelined frames leave room on every CU for the previous frame's sum workgroups:
       // one slot, or two for shards whose traces overlap (N >= 4: each frame's sum is then
       // short enough that the trace does better with it out of its way; shard 1/8 2.23 ->
@@ -1171,8 +1216,11 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
     const int first = pass == 0, last = pass + 1 >= passes;
     if (first && c->copy_pending) HIPCHK(hipStreamWaitEvent(c->stream_sum, c->ev_copy, 0));  // last gather done
     const int sum_kind = wps == 3 && kSkyDefer && nibble ? 1 : 0;
+    // (BVH kernels with 8-B records store attenuation classes: the class table)
     HIPCHK(launch_sum(wps, sum_kind, sum_blocks ? sum_blocks : 1u, c->stream_sum, kp, samples, c->d_running,
-                      c->d_mean, c->d_u8, first, last, ks.att, dc->n));
+                      c->d_mean, c->d_u8, first, last,
+                      bvh_nib ? reinterpret_cast<const float4*>(b + dc->off_acls_att) : ks.att,
+                      bvh_nib ? dc->n_aclass : dc->n));
     HIPCHK(hipEventRecord(c->ev_sum[pass], c->stream_sum));
     summed = pass + 1;
     if (last) break;

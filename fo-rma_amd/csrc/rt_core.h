@@ -335,13 +335,22 @@ __device__ __forceinline__ SphereSeg sphere_seg(float a) {
 // 0.001 in magnitude is below it by either sequence (a numerator under 2^-70 gives
 // |q| < 2^-10 with an absolute error far below the gap), so both reject it. Checked against
 // sphere_root on the device by fr_selftest_ops op 16 (tests/test_gpu_parity.py).
-__device__ __forceinline__ bool sphere_root_fast(V3 c, float radius, V3 o, V3 d, float a, SphereSeg sg,
-                                                 float t_min, float t_max, float& t) {
+// (split in two so that a caller can mark the root step as its own region: the BVH leaf
+// test, tools/isa_sections.py)
+struct SphereDisc {
+  float b, disc;
+};
+__device__ __forceinline__ SphereDisc sphere_disc(V3 c, float radius, V3 o, V3 d, float a) {
   const V3 oc = sub(o, c);
   const float b = dot(oc, d);
   const float cc = dot(oc, oc) - radius * radius;
-  const float disc = b * b - a * cc;
-  if (disc > 0.0f) {
+  return SphereDisc{b, b * b - a * cc};
+}
+// the roots of a sphere test whose discriminant is > 0
+__device__ __forceinline__ bool sphere_roots_fast(SphereDisc q, float a, SphereSeg sg, float t_min, float t_max,
+                                                  float& t) {
+  const float b = q.b, disc = q.disc;
+  {
     float r1, r2;
     const bool fast = static_cast<int>(sg.ok) & static_cast<int>(disc >= 0x1p-96f) & static_cast<int>(disc <= 0x1p126f) &
                       static_cast<int>(__builtin_fabsf(b) <= 0x1p40f);
@@ -359,6 +368,11 @@ __device__ __forceinline__ bool sphere_root_fast(V3 c, float radius, V3 o, V3 d,
     t = c1 ? r1 : r2;
     return c1 || c2;
   }
+}
+__device__ __forceinline__ bool sphere_root_fast(V3 c, float radius, V3 o, V3 d, float a, SphereSeg sg,
+                                                 float t_min, float t_max, float& t) {
+  const SphereDisc q = sphere_disc(c, radius, o, d, a);
+  if (q.disc > 0.0f) return sphere_roots_fast(q, a, sg, t_min, t_max, t);
   return false;
 }
 #endif
@@ -400,6 +414,18 @@ FR_HD Slab slab3_fused(V3 lo, V3 hi, V3 oinv, V3 inv) {
   s.tn = fmax3_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y), fmin_num(s.t0.z, s.t1.z));
   s.tf = fmin3_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y), fmax_num(s.t0.z, s.t1.z));
   return s;
+}
+
+// FR_BOX_FMA (A/B): the box primitive's slab distances as fma(lo, inv, -o inv), one rounding
+// each, with inv clamped to +-2^100 (zero and tiny direction components; see trace_kernel.h),
+// instead of (lo - o) * inv: the same test in one instruction per distinct slab coordinate
+#ifndef FR_BOX_FMA
+#define FR_BOX_FMA 0
+#endif
+FR_HD Slab slab3_box(V3 lo, V3 hi, V3 o, V3 inv, V3 oinv) {
+  if (FR_BOX_FMA) return slab3_fused(lo, hi, oinv, inv);
+  (void)oinv;
+  return slab3(lo, hi, o, inv);
 }
 
 // Root selection: returns true and the accepted t if the box is hit in (t_min, t_max).

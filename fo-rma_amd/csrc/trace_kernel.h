@@ -74,6 +74,13 @@ constexpr uint32_t kMaxWgPerCu = 8;   // 2048 threads per CU / kBlock: the persi
 #ifndef FR_CLAIM_MIN_NIB
 #define FR_CLAIM_MIN_NIB 3
 #endif
+// ... for the BVH kernels with 8-B attenuation-class records (A/B knobs; C5)
+#ifndef FR_KREJ_BVH
+#define FR_KREJ_BVH FR_KREJ
+#endif
+#ifndef FR_CLAIM_MIN_BVH
+#define FR_CLAIM_MIN_BVH FR_CLAIM_MIN
+#endif
 #ifndef FR_NUM_SGPR
 #define FR_NUM_SGPR 96
 #endif
@@ -133,6 +140,9 @@ struct KScene {
   const float4* __restrict__ rec;
   const float4* __restrict__ mat;   // colour rgb, fuzz
   const uint32_t* __restrict__ cls; // effective ScatterClass
+  // attenuation class of each primitive (BVH kernels with 8-B records: the winners are
+  // stored as classes, indices into a table of the scene's <= 15 distinct attenuations)
+  const uint32_t* __restrict__ acls;
   const float4* __restrict__ att;   // attenuation rgb (colour, or 1 for light)
   const float4* __restrict__ bvh;   // BVH nodes, four float4 each (bvh.h)
   const uint32_t* __restrict__ bvh_order;  // primitive index of each leaf slot
@@ -255,7 +265,10 @@ constexpr uint32_t kRecLds = 64;    // whole 64-B records staged in LDS for smal
 #ifndef FR_BVH_STAGE
 #define FR_BVH_STAGE 2
 #endif
-__host__ __device__ constexpr uint32_t stage_samples(bool bvh) { return bvh ? FR_BVH_STAGE : FR_STAGE; }
+// (BVH kernels with 8-B records stage like the list kernels: their LDS holds no unwind stack)
+__host__ __device__ constexpr uint32_t stage_samples(bool bvh, bool nib = false) {
+  return bvh && !nib ? FR_BVH_STAGE : FR_STAGE;
+}
 // FR_BVH_SCALAR_NODES=1: a node step whose walking lanes are all at one node reads it with
 // scalar loads (0, vector loads only: C5 trace 52.9 -> 62.3 ms, the vector memory path
 // returning 64 B per lane per step)
@@ -329,9 +342,12 @@ enum { PF_CLAIM, PF_REJ, PF_HIT, PF_SHADE, PF_END, PF_N };
 // The BVH walk's node step and leaf tests each have a scalar path (every walking lane at one
 // node or leaf) and a vector path, exclusive per entry: they are separate regions (SC_NODES /
 // SC_NODEV, SC_LTESTS / SC_LTESTV), so a static count never adds both paths' instructions to
-// one entry. FR_SECCNT also sums the active lanes of every entry (counters[32 + k]).
+// one entry. SC_LIST: one primitive test of the compiled-in list loops (in a BVH kernel, the
+// in-order fallback for far origins); SC_LROOT: a leaf sphere test's root step (discriminant
+// > 0 on some lane). FR_SECCNT also sums the active lanes of every entry
+// (counters[32 + k]).
 enum { SC_ITER, SC_CLAIM, SC_JIT, SC_NEED, SC_REJ, SC_CAM, SC_SCAT, SC_HIT, SC_SKY, SC_SHADE, SC_END, SC_NODE,
-       SC_LEAF, SC_NODES, SC_NODEV, SC_LTESTS, SC_LTESTV, SC_N, SC_GRAB = SC_N, SC_SETUP, SC_ACC, SC_POSTHIT,
+       SC_LEAF, SC_NODES, SC_NODEV, SC_LTESTS, SC_LTESTV, SC_LIST, SC_LROOT, SC_N, SC_GRAB = SC_N, SC_SETUP, SC_ACC, SC_POSTHIT,
        SC_POSTSHADE, SC_LATCH };
 #if defined(FR_SEC_MARKS) && defined(__HIP_DEVICE_COMPILE__)
 #define SEC(k) asm volatile(";FRSEC " #k)
@@ -529,19 +545,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // leaves idle
   if (FR_TRACE_PRIO) __builtin_amdgcn_s_setprio(FR_TRACE_PRIO);
   extern __shared__ uint32_t lds[];
-  constexpr uint32_t STG = stage_samples(BVH);
   constexpr bool NIB = DEFER == 2;             // 8-B records, winners in a register
+  constexpr uint32_t STG = stage_samples(BVH, NIB);
   constexpr bool DIFFUSE = MAT == 1;           // lambertian scatters only
   constexpr bool SKYD = NIB && kSkyDefer;      // 12-B records {d.y, dot(d, d), winners}
   constexpr uint32_t WPS = NIB && !SKYD ? 2u : 3u;  // words per sample in the buffer
   // list kernels always stage; BVH kernels when the launch gave them the LDS (KF_STAGE)
   constexpr bool RSTG = BVH && FR_BVH_RSTAGE != 0;  // pairs staged in registers
-  const bool staged = STG > 1 && !RSTG && (!BVH || (kp.flags & KF_STAGE) != 0u);
+  const bool staged = STG > 1 && !RSTG && (!BVH || NIB || (kp.flags & KF_STAGE) != 0u);
   float* stage = reinterpret_cast<float*>(lds) + threadIdx.x * (WPS * STG);
   // DEFER kernels (<= kDeferMaxPrims primitives) always hold the attenuations in LDS, and
   // the 8-B-record kernels (<= kNibbleMaxPrims) the records too: compile-time facts there,
   // so their global-load fallbacks are not compiled
-  constexpr bool ATT_LDS = DEFER != 0, REC_LDS = NIB;
+  // (a BVH kernel with 8-B records stores attenuation classes, not primitive indices: its
+  // scenes are larger than these tables)
+  constexpr bool ATT_LDS = DEFER != 0 && !BVH, REC_LDS = NIB && !BVH;
   static_assert(kDeferMaxPrims <= kAttLds && kNibbleMaxPrims <= kRecLds, "LDS staging bounds");
   const uint32_t n_att = ATT_LDS || sc.n <= kAttLds ? sc.n : 0u;
   const uint32_t n_att_st = n_att ? n_att + 1u : 0u;  // with the unit entry
@@ -553,12 +571,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   static_assert(MAXD == 0 || MAXD == 8, "the u16 stack is one 16-B row per lane");
-  static_assert(!DEFER || (MAXD == 8 && !BVH && !MT), "deferred unwind: depth <= 8 list kernels");
+  static_assert(!DEFER || (MAXD == 8 && !MT && (!BVH || (NIB && DIFFUSE))),
+                "deferred unwind: depth <= 8 list kernels, or diffuse BVH kernels with 8-B records");
   uint2* drow = reinterpret_cast<uint2*>(stack) + tid;  // DEFER: this lane's 8 u8 levels
   uint8_t* bstack = reinterpret_cast<uint8_t*>(stack);
   uint4* hrow = reinterpret_cast<uint4*>(stack) + tid;  // this lane's MAXD = 8 levels
   // BVH traversal stack, after the unwind stack: kBvhStack x kBlock u32 (level-major)
-  uint32_t* tstack = stack + (MAXD ? (MAXD * kBlock) / 2u : (kp.max_depth ? kp.max_depth : 1u) * kBlock);
+  // (8-B-record kernels keep their winners in a register: no unwind stack in front)
+  uint32_t* tstack = stack + (NIB ? 0u : MAXD ? (MAXD * kBlock) / 2u : (kp.max_depth ? kp.max_depth : 1u) * kBlock);
   // MAXD > 0 stack entries: with the attenuations in LDS, the entry's byte offset in
   // att_lds (n_att <= kAttLds, so < 2^16), read by the unwind without index arithmetic;
   // otherwise the primitive index
@@ -681,7 +701,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
     // active lane has other work: the claim step (its lane permutes and item setup) then
     // runs for several lanes at once instead of in nearly every iteration for one or two.
     // Only when work starts changes, never what a sample computes (results bit-identical).
-    constexpr uint32_t CLAIM_MIN = NIB ? FR_CLAIM_MIN_NIB : FR_CLAIM_MIN;
+    constexpr uint32_t CLAIM_MIN = NIB ? (BVH ? FR_CLAIM_MIN_BVH : FR_CLAIM_MIN_NIB) : FR_CLAIM_MIN;
     if (m && (CLAIM_MIN <= 1 || lanes_in(m) >= CLAIM_MIN || m == __ballot(1))) {
       SEC(SC_CLAIM);
       // 0. claim work items: the free lanes take consecutive items of the wave's batch;
@@ -907,6 +927,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       const int rok = static_cast<int>(recip_nr_ok(d.x)) & static_cast<int>(recip_nr_ok(d.y)) &
                       static_cast<int>(recip_nr_ok(d.z));
       if (!rok) inv = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+      if (FR_BOX_FMA) {
+        // the box test's reciprocal clamped to +-2^100 (only components below 2^-100 reach it)
+        inv = V3{__builtin_amdgcn_fmed3f(inv.x, -0x1p100f, 0x1p100f), __builtin_amdgcn_fmed3f(inv.y, -0x1p100f, 0x1p100f),
+                 __builtin_amdgcn_fmed3f(inv.z, -0x1p100f, 0x1p100f)};
+      }
+      const V3 boinv{o.x * inv.x, o.y * inv.y, o.z * inv.z};  // (FR_BOX_FMA box tests only)
       const float a_dd = dot(d, d);
 #ifndef FR_SPHERE_IEEE
       const SphereSeg ssg = sphere_seg(a_dd);  // unused (removed) in kernels without spheres
@@ -1050,12 +1076,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               if (k == FR_SPHERE) {
                 const float4 g = r[0];
 #ifndef FR_SPHERE_IEEE
-                h = sphere_root_fast(xyz(g), g.w, o, d, a_dd, ssg, 0.001f, tmax, t);
+                const SphereDisc q = sphere_disc(xyz(g), g.w, o, d, a_dd);
+                if (q.disc > 0.0f) {
+                  SEC(SC_LROOT);
+                  h = sphere_roots_fast(q, a_dd, ssg, 0.001f, tmax, t);
+                }
 #else
                 h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, tmax, t);
 #endif
               } else if (k == FR_AABB) {
-                h = slab_root(slab3(xyz(r[0]), xyz(r[1]), o, inv), 0.001f, tmax, t);
+                h = slab_root(slab3_box(xyz(r[0]), xyz(r[1]), o, inv, boinv), 0.001f, tmax, t);
               } else if (k == FR_TRIANGLE) {
                 h = tri_root(xyz(r[0]), xyz(r[1]), xyz(r[2]), o, d, 0.001f, tmax, t);
               } else if (k == FR_OBB) {
@@ -1115,7 +1145,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         float t = 0.0f;
         bool h = false;
         if constexpr (K == FR_AABB) {
-          h = slab_root(slab3(xyz(r4[0]), xyz(r4[1]), o, inv), 0.001f, closest, t);
+          h = slab_root(slab3_box(xyz(r4[0]), xyz(r4[1]), o, inv, boinv), 0.001f, closest, t);
         } else if constexpr (K == FR_SPHERE) {
           const float4 g = r4[0];
 #ifndef FR_SPHERE_IEEE
@@ -1150,7 +1180,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
         }
 #endif
       };
-      auto test_one = [&](auto kind_tag, uint32_t i) { test_rec(kind_tag, i, rec_at(sc.rec, i)); };
+      auto test_one = [&](auto kind_tag, uint32_t i) {
+        SEC(SC_LIST);
+        test_rec(kind_tag, i, rec_at(sc.rec, i));
+      };
       typedef std::integral_constant<uint32_t, FR_AABB> TagAabb;
       typedef std::integral_constant<uint32_t, FR_SPHERE> TagSphere;
 #ifdef FR_JIT_N
@@ -1181,7 +1214,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       } else
 #endif
 #ifndef FR_NO_UNROLL_NIB
-      if constexpr (NIB && KS != KS_ANY) {
+      if constexpr (NIB && !BVH && KS != KS_ANY) {
         // <= kNibbleMaxPrims primitives: the tests unrolled over the compile-time bound with
         // an exit at n, each index an inline constant (the winner select needs no index
         // register) and each record at a constant offset. C3 trace 17.45 -> 17.29 ms as a
@@ -1286,7 +1319,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           const uint32_t kb = KS == KS_AABB ? FR_AABB : KS == KS_SPHERE ? FR_SPHERE : __float_as_uint(b3.w);
           V3 n;
           if (kb == FR_AABB) {
-            n = slab_normal(slab3(xyz(b0), xyz(b1), o, inv), closest, d);
+            n = slab_normal(slab3_box(xyz(b0), xyz(b1), o, inv, boinv), closest, d);
           } else if (kb == FR_SPHERE) {
             n = divs(sub(pw, xyz(b0)), b0.w);
           } else if (kb == FR_PLANE) {
@@ -1313,7 +1346,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           if (c != SC_NONE && (DIFFUSE || c != SC_DIELECTRIC)) need = NEED_SPHERE;
           // a lambertian scatter always continues the path (sphere.rs:84-89): with only those
           // (and stubs, which end it above) the winner is pushed here, not held to the scatter
-          if (NIB && DIFFUSE && c != SC_NONE) push(static_cast<uint32_t>(best));
+          if (NIB && DIFFUSE && c != SC_NONE) {
+            if (BVH)
+              push(buf_load1(sc.acls, 4u * static_cast<uint32_t>(best)));  // the winner's attenuation class
+            else
+              push(static_cast<uint32_t>(best));
+          }
           if (!DIFFUSE && c == SC_DIELECTRIC) {
             // one draw, no rejection loop (sphere.rs:107-145)
             d = scatter_dielectric(din, n, rng);

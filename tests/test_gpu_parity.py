@@ -862,6 +862,39 @@ def test_bvh_matches_list_order_loop(gpu, seed, planes, depth, monkeypatch):
     assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
 
 
+@pytest.mark.parametrize("seed,planes,k,depth", [(0, 0, 1, 8), (1, 0, 7, 8), (2, 3, 15, 8), (3, 0, 16, 8),
+                                                 (6, 12, 5, 8), (4, 1, 3, 5)])
+def test_bvh_attenuation_class_records(gpu, seed, planes, k, depth, monkeypatch):
+    """Diffuse BVH scenes with at most 15 distinct attenuations (lambertian colours, light's
+    1) run the BVH kernel with 8-B records: a path's winners stored as attenuation classes
+    and multiplied out by sum_nib_kernel from the class table; 16 classes
+    keep the unwind in the trace kernel. Every kind, stubs, planes between BVH runs and
+    list-order ties: against the oracle, the unwinding BVH kernel (FR_DEFER=0) and the
+    in-order loop (FR_BVH=0), bit for bit."""
+    w, h, spp = 48, 32, 3
+    prims = bvh_scene(seed, planes=planes)
+    r = np.random.default_rng(100 + seed)
+    pal = r.uniform(0.1, 1.0, (k, 3)).astype(np.float32)
+    for q in prims:
+        q["material"] = S.LIGHT if (k < 15 and r.uniform() < 0.1) else S.LAMBERTIAN
+        q["color"] = pal[int(r.integers(0, k))]
+        q["fuzz"] = np.float32(0.0)
+    sc = gpu.Scene.from_prims(prims)
+    cam, ocam = gpu.camera_new(w, h), O.camera_new(w, h)
+    gpu.camera_orbit(cam, (0.3 * seed, 0.05 * seed, 1.5))
+    O.camera_orbit(ocam, (0.3 * seed, 0.05 * seed, 1.5))
+    monkeypatch.delenv("FR_DEFER", raising=False)
+    mean, u8, st = gpu.render(sc, cam, w, h, spp, depth, seed=91 + seed)
+    omean, ou8, ocnt, _ = O.render(prims, ocam, w, h, spp, depth, seed=91 + seed, threads=8)
+    assert_parity(mean, u8, st, omean, ou8, ocnt)
+    for env in (("FR_DEFER", "0"), ("FR_BVH", "0")):
+        monkeypatch.setenv(*env)
+        m0, u0, st0 = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=91 + seed)
+        assert np.array_equal(m0.view(np.uint32), mean.view(np.uint32)) and np.array_equal(u0, u8), env
+        assert (st0["segments"], st0["hits"]) == (st["segments"], st["hits"]), env
+        monkeypatch.delenv(env[0])
+
+
 @pytest.mark.parametrize("layout", ["same", "line", "pairs"])
 def test_bvh_degenerate_trees_keep_list_order_ties(gpu, layout, monkeypatch):
     """Trees the SAH sweep cannot separate: 64 identical spheres (every hit a tie: the list's
@@ -888,19 +921,26 @@ def test_bvh_degenerate_trees_keep_list_order_ties(gpu, layout, monkeypatch):
     assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
 
 
-def test_bvh_far_origins_from_stale_plane_records(gpu, monkeypatch):
+@pytest.mark.parametrize("classes", [None, 4])
+def test_bvh_far_origins_from_stale_plane_records(gpu, classes, monkeypatch):
     """Planes listed after the other primitives, small and in every orientation: a plane
     whose denominator gate passes (plane.rs:26) but whose bounds test fails still writes
     t (plane.rs:27-40), so the scatter origin p = o + t_stale d of the earlier winner can
     lie thousands of scene extents away, where the BVH's node cull is not conservative.
     Waves with such an origin walk the list in order (render.hip); the image must equal
-    the list-order loop (FR_BVH=0) and the oracle bit for bit."""
+    the list-order loop (FR_BVH=0) and the oracle bit for bit. classes=4: the scene made
+    diffuse with four colours, so the BVH kernel with attenuation-class records runs it."""
     prims = bvh_scene(7, n=300)[:-1]  # no ground sphere: the scene extent stays small
     r = np.random.default_rng(7)
     for _ in range(16):
         o = r.standard_normal(3)
         c = r.uniform(-6, 6, 3) + np.array([0, 0, -8.0])
         prims.append(S.plane(c, o, r.uniform(0.2, 1.0, 3), int(r.integers(0, 2)), r.uniform(0.1, 1.0, 3), 0.3))
+    if classes:
+        pal = r.uniform(0.1, 1.0, (classes, 3)).astype(np.float32)
+        for q in prims:
+            q["material"] = S.LAMBERTIAN
+            q["color"] = pal[int(r.integers(0, classes))]
     assert bvh_cost(prims) >= 48
     w, h, spp, depth = 48, 32, 6, 8
     cam = gpu.camera_new(w, h)

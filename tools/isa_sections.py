@@ -29,7 +29,7 @@ CSRC = os.path.join(ROOT, "fo-rma_amd", "csrc")
 # (the BVH walk's scalar and vector paths are separate regions: SC_NODES / SC_NODEV after the
 # node step's common head SC_NODE, SC_LTESTS / SC_LTESTV for one leaf test)
 REGIONS = ["SC_ITER", "SC_CLAIM", "SC_JIT", "SC_NEED", "SC_REJ", "SC_CAM", "SC_SCAT", "SC_HIT", "SC_SKY", "SC_SHADE",
-           "SC_END", "SC_NODE", "SC_LEAF", "SC_NODES", "SC_NODEV", "SC_LTESTS", "SC_LTESTV"]
+           "SC_END", "SC_NODE", "SC_LEAF", "SC_NODES", "SC_NODEV", "SC_LTESTS", "SC_LTESTV", "SC_LIST", "SC_LROOT"]
 # marker-only regions: the counted region whose entries they share
 DERIVED = {"SC_SETUP": "SC_CLAIM", "SC_ACC": "SC_NEED", "SC_POSTHIT": "SC_HIT", "SC_POSTSHADE": "SC_ITER",
            "SC_LATCH": "SC_ITER"}
@@ -98,8 +98,9 @@ def count_regions(asm):
     region of the block before it in the layout, except: blocks of the rejection loop
     (the loops nested in the lane loop) are SC_REJ / SC_LENS; lane-loop blocks laid out before the
     loop header are SC_LATCH; unmarked blocks with a full IEEE division (v_div_fixup: the
-    reciprocal guard's fallback) are RARE (not entered in a normal frame); blocks after
-    the lane loop are EPILOGUE."""
+    reciprocal guard's and the sky parameter's fallbacks) are RARE (not entered in a normal
+    frame); blocks after the lane loop are EPILOGUE. `instances` counts a region's marker
+    copies (unrolled loops)."""
     lines = open(asm).read().splitlines()
     blocks, cur, in_fn, meta = [], None, False, {}
     for ln in lines:
@@ -157,10 +158,13 @@ def count_regions(asm):
         for h, reg in inner.items():
             if ("Header=" + h + " ") in (b["cmt"] + " ") and not b["mark"]:
                 r = reg
-        if not b["mark"] and "v_div_fixup_f32" in b["ops"] and r not in ("SC_SKY",):
+        # (the sky parameter's IEEE fallback too: its fast path is the default since round 5)
+        if not b["mark"] and "v_div_fixup_f32" in b["ops"]:
             r = "RARE"
-        t = tab.setdefault(r, {"valu": 0, "salu": 0, "lds": 0, "mem": 0, "blocks": 0})
+        t = tab.setdefault(r, {"valu": 0, "salu": 0, "lds": 0, "mem": 0, "blocks": 0, "instances": 0})
         t["blocks"] += 1
+        if b["mark"]:
+            t["instances"] += 1  # copies of the marker (an unrolled loop repeats its region)
         for op in b["ops"]:
             kind = ("valu" if op.startswith("v_") else "salu" if op.startswith("s_") else
                     "lds" if op.startswith("ds_") else "mem")
@@ -174,10 +178,15 @@ def combine(static_path, seccnt_path, segments, valu_measured, grabs=0):
     counts = json.loads(line.split("FR_SECCNT", 1)[1])
     lanes_l = [ln for ln in open(seccnt_path) if "FR_SECLANES" in ln]
     lanes = json.loads(lanes_l[-1].split("FR_SECLANES", 1)[1]) if lanes_l else [0] * len(counts)
+    # a build with fewer regions (older SC_* lists) reads 0 for the later ones
+    counts += [0] * (len(REGIONS) - len(counts))
+    lanes += [0] * (len(REGIONS) - len(lanes))
     tab = st["regions"]
     rows, tot = [], 0.0
     for name in REGIONS + list(DERIVED) + ["SC_GRAB"]:
-        v = tab.get(name, {}).get("valu", 0)
+        # VALU per entry: a region's instructions over its marker's copies (each copy of an
+        # unrolled loop body counts its own entries)
+        v = tab.get(name, {}).get("valu", 0) / max(1, tab.get(name, {}).get("instances", 1))
         if name in REGIONS:
             n, ln = counts[REGIONS.index(name)], lanes[REGIONS.index(name)]
         elif name in DERIVED:
