@@ -422,6 +422,13 @@ FR_HD Slab slab3_fused(V3 lo, V3 hi, V3 oinv, V3 inv) {
 #ifndef FR_BOX_FMA
 #define FR_BOX_FMA 0
 #endif
+constexpr float kBoxInvClamp = 0x1p100f;
+FR_HD float box_inv_clamp(float inv) { return fmin_num(fmax_num(inv, -kBoxInvClamp), kBoxInvClamp); }
+// recip_nr's range narrowed to |x| >= 2^-100: there RN(1 / x) is within the clamp
+FR_HD bool recip_box_ok(float x) {
+  const float ax = __builtin_fabsf(x);
+  return (ax >= 0x1p-100f) & (ax < 0x1p126f);
+}
 FR_HD Slab slab3_box(V3 lo, V3 hi, V3 o, V3 inv, V3 oinv) {
   if (FR_BOX_FMA) return slab3_fused(lo, hi, oinv, inv);
   (void)oinv;

@@ -924,13 +924,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       ++nseg;
       V3 inv{recip_nr(d.x), recip_nr(d.y), recip_nr(d.z)};
       // (non-short-circuit: one branch to the rare fallback instead of three nested ones)
-      const int rok = static_cast<int>(recip_nr_ok(d.x)) & static_cast<int>(recip_nr_ok(d.y)) &
-                      static_cast<int>(recip_nr_ok(d.z));
-      if (!rok) inv = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-      if (FR_BOX_FMA) {
-        // the box test's reciprocal clamped to +-2^100 (only components below 2^-100 reach it)
-        inv = V3{__builtin_amdgcn_fmed3f(inv.x, -0x1p100f, 0x1p100f), __builtin_amdgcn_fmed3f(inv.y, -0x1p100f, 0x1p100f),
-                 __builtin_amdgcn_fmed3f(inv.z, -0x1p100f, 0x1p100f)};
+      // FR_BOX_FMA: the box test's reciprocal is RN(1 / d) clamped to +-2^100 (rt_core.h
+      // box_inv): recip_nr's range is narrowed to |d| >= 2^-100, where the clamp is the
+      // identity, and the fallback clamps
+      const int rok = FR_BOX_FMA ? static_cast<int>(recip_box_ok(d.x)) & static_cast<int>(recip_box_ok(d.y)) &
+                                       static_cast<int>(recip_box_ok(d.z))
+                                 : static_cast<int>(recip_nr_ok(d.x)) & static_cast<int>(recip_nr_ok(d.y)) &
+                                       static_cast<int>(recip_nr_ok(d.z));
+      if (!rok) {
+        inv = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        if (FR_BOX_FMA) inv = V3{box_inv_clamp(inv.x), box_inv_clamp(inv.y), box_inv_clamp(inv.z)};
       }
       const V3 boinv{o.x * inv.x, o.y * inv.y, o.z * inv.z};  // (FR_BOX_FMA box tests only)
       const float a_dd = dot(d, d);
@@ -1034,9 +1037,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                                 __builtin_amdgcn_ballot_w64(sr.tf >= 0.001f) & __builtin_amdgcn_ballot_w64(sr.tn <= closest);
                 const Mask mgol = ml & (__builtin_amdgcn_ballot_w64(sl.tn <= sr.tn) | ~mr);
                 const Mask many = ml | mr;
-                tstack[tso] = lane_sel(mgol, cr, cl);
+                // near = mgol ? cl : cr and far = the other, as xors with cl ^ cr: in the scalar
+                // step cl and cr are SGPRs, and a select between two SGPRs needs one of them
+                // copied to a VGPR first (one scalar operand per VALU instruction)
+                const uint32_t cx = cl ^ cr;
+                const uint32_t near = cl ^ lane_sel(mgol, 0u, cx);
+                tstack[tso] = near ^ cx;  // the far child
                 const uint32_t tpop = lane_sel(many | mempty, tso, tdown);
-                ref = lane_sel(many, lane_sel(mgol, cl, cr), lane_sel(mempty, kBvhEnd, top));
+                ref = lane_sel(many, near, lane_sel(mempty, kBvhEnd, top));
                 tso = lane_sel(ml & mr, tso + kBlock, tpop);
               };
 #if FR_BVH_SCALAR_NODES

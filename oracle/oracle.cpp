@@ -376,12 +376,50 @@ struct BoxBase : Hitable {
   }
 };
 
+#ifndef OR_BOX_FMA
+#define OR_BOX_FMA 0
+#endif
 struct Aabb : BoxBase {
   Vec3 mn, mx;
+  // OR_BOX_FMA: the axis-aligned box's slab distances as fmaf(lo_k, inv_k, -(o_k * inv_k))
+  // with inv_k = RN(1 / d_k) clamped to [-2^100, 2^100] (fmaxf, then fminf), the rest as
+  // slabs() (the product's FR_BOX_FMA)
+  static bool slabs_fma(Vec3 lo, Vec3 hi, Vec3 o, Vec3 d, float t_min, float t_max, float& t, Vec3& n_local) {
+    float t0[3], t1[3], nr[3], fr[3];
+    for (int k = 0; k < 3; ++k) {
+      const float inv = fminf(fmaxf(1.0f / pick(d, k), -0x1p100f), 0x1p100f);
+      const float oinv = pick(o, k) * inv;
+      t0[k] = fmaf(pick(lo, k), inv, -oinv);
+      t1[k] = fmaf(pick(hi, k), inv, -oinv);
+      nr[k] = fminf(t0[k], t1[k]);
+      fr[k] = fmaxf(t0[k], t1[k]);
+    }
+    const float tn = fmaxf(fmaxf(nr[0], nr[1]), nr[2]);
+    const float tf = fminf(fminf(fr[0], fr[1]), fr[2]);
+    if (!(tn < tf)) return false;
+    int k;
+    float s;
+    if (tn > t_min && tn < t_max) {
+      t = tn;
+      k = nr[0] == tn ? 0 : (nr[1] == tn ? 1 : 2);
+      s = pick(d, k) > 0.0f ? -1.0f : 1.0f;
+    } else if (tf > t_min && tf < t_max) {
+      t = tf;
+      k = fr[0] == tf ? 0 : (fr[1] == tf ? 1 : 2);
+      s = pick(d, k) > 0.0f ? 1.0f : -1.0f;
+    } else {
+      return false;
+    }
+    n_local = Vec3();
+    (k == 0 ? n_local.x : k == 1 ? n_local.y : n_local.z) = s;
+    return true;
+  }
   bool hit(Ray ray, float t_min, float t_max, HitRecord& rec) const override {
     float t;
     Vec3 n;
-    if (!slabs(mn, mx, ray.origin(), ray.direction(), t_min, t_max, t, n)) return false;
+    const bool h = OR_BOX_FMA ? slabs_fma(mn, mx, ray.origin(), ray.direction(), t_min, t_max, t, n)
+                              : slabs(mn, mx, ray.origin(), ray.direction(), t_min, t_max, t, n);
+    if (!h) return false;
     rec.t = t;
     rec.p = ray.point_at(t);
     rec.normal = n;
