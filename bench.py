@@ -144,6 +144,7 @@ def algorithmic_flops(c, counts, prim_kinds, pixels, scatter="Lambert"):
     winner-kind and scatter-class terms use the scene's single kind and class (scene_08:
     boxes, lambertian)."""
     seg = c["kFlopSegment"] + (c["kFlopSegmentSphere"] if prim_kinds.get("Sphere") else 0.0)
+    seg += c.get("kFlopSegmentBox", 0.0) if prim_kinds.get("Box") else 0.0
     seg += sum(n * c[f"kFlopTest{k}"] for k, n in prim_kinds.items())
     (kind,) = [k for k, n in prim_kinds.items() if n]
     return (counts["segments"] * seg + counts["hits"] * c[f"kFlopHit{kind}"]

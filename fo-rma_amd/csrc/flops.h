@@ -20,12 +20,15 @@ namespace fr {
 
 // per segment: 1/d per axis (recip_nr, render.hip closest-hit setup)
 constexpr double kFlopSegment = 3;
+// ... plus o * inv per axis when the scene has axis-aligned boxes (their slab distances are
+// fma(lo, inv, -(o inv)), rt_core.h slab3_box; an fma counts as two flops)
+constexpr double kFlopSegmentBox = 3;
 // ... plus a = dot(d, d) when the scene has spheres (sphere_root's loop-invariant a)
 constexpr double kFlopSegmentSphere = 5;
 
 // closest-hit tests, per primitive per segment
-// box, slab3 + slab_root: (lo - o) * inv, (hi - o) * inv per axis (12), per-axis min and
-// max (6), tn = max of 3 (2), tf = min of 3 (2)
+// box, slab3_box + slab_root: fma(lo, inv, -(o inv)), fma(hi, inv, -(o inv)) per axis (12),
+// per-axis min and max (6), tn = max of 3 (2), tf = min of 3 (2)
 constexpr double kFlopTestBox = 22;
 // sphere_root (sphere.rs:23-51): oc (3), b = dot (5), c = dot - r*r (7), disc (3); on
 // disc > 0 also sqrt, -b -+ sq, two divides (5): counted as the miss path

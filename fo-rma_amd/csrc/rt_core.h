@@ -416,11 +416,14 @@ FR_HD Slab slab3_fused(V3 lo, V3 hi, V3 oinv, V3 inv) {
   return s;
 }
 
-// FR_BOX_FMA (A/B): the box primitive's slab distances as fma(lo, inv, -o inv), one rounding
-// each, with inv clamped to +-2^100 (zero and tiny direction components; see trace_kernel.h),
-// instead of (lo - o) * inv: the same test in one instruction per distinct slab coordinate
+// The build-defined box's slab distances: fma(lo, inv, -(o inv))
+// with inv = RN(1 / d) clamped to +-2^100, one rounding per distance instead of the two of
+// (lo - o) * inv, and one instruction per distinct slab coordinate of the scene kernel (o inv
+// is per segment): C3 14.84 -> 14.48 ms per streamed frame (profiles/r06e_ab_boxfma.log).
+// The clamp keeps zero and tiny direction components finite (inf * lo - inf * o would be
+// NaN). FR_BOX_FMA=0 builds the round-5 form (A/B; the oracle's OR_BOX_FMA=0 matches it).
 #ifndef FR_BOX_FMA
-#define FR_BOX_FMA 0
+#define FR_BOX_FMA 1
 #endif
 constexpr float kBoxInvClamp = 0x1p100f;
 FR_HD float box_inv_clamp(float inv) { return fmin_num(fmax_num(inv, -kBoxInvClamp), kBoxInvClamp); }

@@ -326,7 +326,8 @@ struct Stub : Hitable {
 };
 
 // ---- build-defined box, restated from its written spec ------
-// Slabs per axis k: t0 = (lo_k - o_k) * (1/d_k), t1 = (hi_k - o_k) * (1/d_k);
+// Slabs per axis k: t0 = (lo_k - o_k) * (1/d_k), t1 = (hi_k - o_k) * (1/d_k) (the oriented
+// box; the axis-aligned one computes them as Aabb::slabs_fma does, OR_BOX_FMA);
 // near_k = fminf(t0, t1), far_k = fmaxf(t0, t1) (C99 fmin/fmax: NaN-ignoring);
 // tn = fmaxf(fmaxf(near_x, near_y), near_z), tf = fminf(fminf(far_x, far_y), far_z).
 // Hit iff tn < tf; then the near root if it is in (t_min, t_max), else the far root
@@ -377,7 +378,7 @@ struct BoxBase : Hitable {
 };
 
 #ifndef OR_BOX_FMA
-#define OR_BOX_FMA 0
+#define OR_BOX_FMA 1  // the box definition since round 6; 0: round 5's
 #endif
 struct Aabb : BoxBase {
   Vec3 mn, mx;
