@@ -1018,8 +1018,13 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       if (cap_blocks >= static_cast<uint64_t>(k) * nblocks) nfs = k;
   const bool fpipe = nfs > 0;
   const uint64_t grid_lanes = static_cast<uint64_t>(c->num_cus) * (kMaxWgPerCu - 1u) * kBlock;
+  // (round 6: below three slots per grid lane, so N = 2 shards of a 1080p frame overlap too;
+  // at N = 1 a launch's own HIP-event time stays the launch's, and the gain measured 0.3 %)
   const bool fpipe_overlap =
-      fpipe && (fp_env && *fp_env ? strcmp(fp_env, "2") == 0 : static_cast<uint64_t>(kp.P) < 2u * grid_lanes);
+      fpipe && (fp_env && *fp_env ? strcmp(fp_env, "2") == 0 : static_cast<uint64_t>(kp.P) < 3u * grid_lanes);
+  // The previous frame of this context still running (its end event pending): frames are
+  // being streamed, and this trace shares the CUs with the previous frame's trace or sum
+  const bool prev_in_flight = c->pending && hipEventQuery(c->ev1) == hipErrorNotReady;
   const size_t slot_bytes = per_block * nb_pass;
   // a new layout (slot count or size, or not pipelined): every earlier frame must have been
   // summed before this one reuses the buffers; in one layout only this slot's last user
@@ -1182,12 +1187,16 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       Grid grid{(static_cast<uint64_t>(kp.n_items) + kBlock - 1u) / kBlock, c->num_cus, &c->occupancy, &blocks,
                 use_bvh && !nibble && stage_n > 1 && !FR_BVH_RSTAGE ? kBlock * stage_n * 3 * sizeof(float) : 0u};
       // pipelined frames leave room on every CU for the previous frame's sum workgroups:
-      // one slot, or two for shards whose traces overlap (N >= 4: each frame's sum is then
-      // short enough that the trace does better with it out of its way; shard 1/8 2.23 ->
-      // 2.18 ms per frame, 1/4 4.25 -> 4.19; at N = 1 two cost 6 %)
+      // one slot at N = 1 (two cost 6 %); until round 5 two for shards
+      // whose traces overlap (shard 1/8 2.23 -> 2.18 ms per frame against one).
+      // Round 6: overlapping traces of streamed frames take half the CU slots each (reserve
+      // 4 of 8), so two frames' traces run side by side and each fills the other's drain:
+      // shards of 8 stream at 1.81 ms per frame against 1.90 with reserve 2, of 4 at 3.60
+      // against 3.70, of 2 at 7.21 against 7.30 (profiles/r06i_*, r06j_*). A frame whose
+      // predecessor has finished shares the CUs with nothing: no reserve.
       if (fpipe) {
         const char* r = getenv("FR_FRAME_PIPE_RESERVE");
-        grid.reserve = r ? static_cast<uint32_t>(atoi(r)) : fpipe_overlap ? 2u : 1u;
+        grid.reserve = r ? static_cast<uint32_t>(atoi(r)) : !prev_in_flight ? 0u : fpipe_overlap ? 4u : 1u;
       }
       unsigned long long* wcnt = c->d_wcnt + static_cast<size_t>(slot) * 3 * kMaxWgPerCu * (kBlock / 64u) * c->num_cus;
       kw.wave_counters = wcnt;

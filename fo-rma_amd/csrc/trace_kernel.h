@@ -1027,10 +1027,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               // way (a node at depth d has at most d entries below it, d < kBvhStack) and the
               // index moves only on a push or pop. (A ballot of an & of compares went through
               // a 0/1 VGPR and a compare: the compares' own masks are combined with SALU ops.)
-              auto node_step = [&](const float4 na, const float4 nb, const float4 nc, const uint32_t cl,
-                                   const uint32_t cr) {
-                const Slab sl = slab3_fused(xyz(na), xyz(nb), oinv, invc);
-                const Slab sr = slab3_fused(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, oinv, invc);
+              auto node_pick = [&](const Slab& sl, const Slab& sr, const uint32_t cl, const uint32_t cr) {
                 const Mask ml = __builtin_amdgcn_ballot_w64(sl.tn <= sl.tf) &
                                 __builtin_amdgcn_ballot_w64(sl.tf >= 0.001f) & __builtin_amdgcn_ballot_w64(sl.tn <= closest);
                 const Mask mr = __builtin_amdgcn_ballot_w64(sr.tn <= sr.tf) &
@@ -1047,6 +1044,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                 ref = lane_sel(many, near, lane_sel(mempty, kBvhEnd, top));
                 tso = lane_sel(ml & mr, tso + kBlock, tpop);
               };
+              auto node_step = [&](const float4 na, const float4 nb, const float4 nc, const uint32_t cl,
+                                   const uint32_t cr) {
+                node_pick(slab3_fused(xyz(na), xyz(nb), oinv, invc),
+                          slab3_fused(V3{na.w, nc.x, nc.y}, V3{nb.w, nc.z, nc.w}, oinv, invc), cl, cr);
+              };
 #if FR_BVH_SCALAR_NODES
               const uint32_t ref0 = __builtin_amdgcn_readfirstlane(ref);
               if (__ballot(ref != ref0) == 0) {
@@ -1054,9 +1056,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                 // rays of one tile): scalar loads, the slab arithmetic on SGPR operands (the
                 // distinct asm ends keep the two paths from being merged over copies of the
                 // node into VGPRs)
-                SEC(SC_NODES);
                 const RecRef nd = rec_at(sc.bvh, ref0);
                 const float4 r = nd[3];
+                SEC(SC_NODES);
                 node_step(nd[0], nd[1], nd[2], __float_as_uint(r.x), __float_as_uint(r.y));
                 asm volatile("; bvh node step: scalar");
               } else
