@@ -493,6 +493,9 @@ struct fr_ctx {
   fr_params last{};
   uint32_t last_n = 0;
   bool pending = false;
+  // the last render was enqueued while the one before it still ran (frames streamed): the
+  // next render reserves slots for overlapping even if it finds the device idle (render_ctx)
+  bool streaming = false;
   std::chrono::steady_clock::time_point t0;
   // fr_ctx_trace_log: event pairs around every trace launch since the log was enabled,
   // across renders (ev_trace holds only the last render's), so a caller streaming K
@@ -1024,7 +1027,11 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       fpipe && (fp_env && *fp_env ? strcmp(fp_env, "2") == 0 : static_cast<uint64_t>(kp.P) < 3u * grid_lanes);
   // The previous frame of this context still running (its end event pending): frames are
   // being streamed, and this trace shares the CUs with the previous frame's trace or sum
-  const bool prev_in_flight = c->pending && hipEventQuery(c->ev1) == hipErrorNotReady;
+  const bool prev_in_flight = !dry && c->pending && hipEventQuery(c->ev1) == hipErrorNotReady;
+  // one frame of memory: the first frame of a burst that follows a host wait (a timed region
+  // after its warm-up) still overlaps; a caller that waits for every frame (update()) never does
+  const bool stream_mode = prev_in_flight || c->streaming;
+  if (!dry) c->streaming = prev_in_flight;
   const size_t slot_bytes = per_block * nb_pass;
   // a new layout (slot count or size, or not pipelined): every earlier frame must have been
   // summed before this one reuses the buffers; in one layout only this slot's last user
@@ -1196,7 +1203,7 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
       // predecessor has finished shares the CUs with nothing: no reserve.
       if (fpipe) {
         const char* r = getenv("FR_FRAME_PIPE_RESERVE");
-        grid.reserve = r ? static_cast<uint32_t>(atoi(r)) : !prev_in_flight ? 0u : fpipe_overlap ? 4u : 1u;
+        grid.reserve = r ? static_cast<uint32_t>(atoi(r)) : !stream_mode ? 0u : fpipe_overlap ? 4u : 1u;
       }
       unsigned long long* wcnt = c->d_wcnt + static_cast<size_t>(slot) * 3 * kMaxWgPerCu * (kBlock / 64u) * c->num_cus;
       kw.wave_counters = wcnt;

@@ -77,3 +77,16 @@ def test_n_gt_1_line_checks_its_stitched_frame_against_n1():
     bad[y, 1, 2] = np.nextafter(bad[y, 1, 2], np.float32(2.0))
     r = bench.compare_with_n1(bad, whole)
     assert not r["frame_matches_n1"] and r["frame_sha256_16"] != r["n1_frame_sha256_16"]
+
+
+def test_flop_model_counts_the_box_segment_term():
+    """flops.h's constants as bench.py reads them: a box scene pays o * inv once per segment
+    (3 flops, the fma slab form) on top of 22 per box test; a sphere scene
+    pays a = dot(d, d) (5) instead."""
+    c = bench.flop_constants()
+    assert c["kFlopSegment"] == 3 and c["kFlopSegmentBox"] == 3 and c["kFlopTestBox"] == 22
+    counts = {"segments": 10, "hits": 0, "scatters": 0, "samples": 0}
+    box = bench.algorithmic_flops(c, counts, {"Box": 6}, 0)
+    sph = bench.algorithmic_flops(c, counts, {"Sphere": 2}, 0)
+    assert box == 10 * (3 + 3 + 6 * 22) + 10 * c["kFlopSky"]
+    assert sph == 10 * (3 + 5 + 2 * 18) + 10 * c["kFlopSky"]
