@@ -895,6 +895,26 @@ def test_bvh_attenuation_class_records(gpu, seed, planes, k, depth, monkeypatch)
         monkeypatch.delenv(env[0])
 
 
+def test_bvh_attenuation_class_records_across_passes(gpu, monkeypatch):
+    """The class records through the multi-pass path (a sample buffer of one block per pass:
+    traces alternate between two streams, sum_nib_kernel carries the running sum): the same
+    bits as one pass, for a diffuse three-class BVH scene."""
+    w, h, spp, depth = 256, 128, 40, 8
+    prims = bvh_scene(9)
+    r = np.random.default_rng(109)
+    pal = r.uniform(0.1, 1.0, (3, 3)).astype(np.float32)
+    for q in prims:
+        q["material"] = S.LAMBERTIAN
+        q["color"] = pal[int(r.integers(0, 3))]
+    cam = gpu.camera_new(w, h)
+    one = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=5)
+    monkeypatch.setenv("FR_SAMPLE_BUFFER_GB", "0.001")  # 1 MiB: one 4-MiB block per pass
+    many = gpu.render(gpu.Scene.from_prims(prims), cam, w, h, spp, depth, seed=5)
+    assert many[2]["trace_launches"] == 3, many[2]
+    assert np.array_equal(many[0].view(np.uint32), one[0].view(np.uint32)) and np.array_equal(many[1], one[1])
+    assert (many[2]["segments"], many[2]["hits"]) == (one[2]["segments"], one[2]["hits"])
+
+
 @pytest.mark.parametrize("layout", ["same", "line", "pairs"])
 def test_bvh_degenerate_trees_keep_list_order_ties(gpu, layout, monkeypatch):
     """Trees the SAH sweep cannot separate: 64 identical spheres (every hit a tie: the list's
