@@ -99,6 +99,8 @@ struct Builder {
   std::vector<uint32_t>& slots;    // item id per leaf slot, relative to slot 0 of this tree
   float pad;
   uint32_t leaf_max;
+  uint32_t leaf_cap = kBvhLeafCountMax;  // SAH-terminated leaves: at most this many items
+  double sah_ct = 0.0;                   // node step cost in leaf tests (0: leaves of leaf_max)
   uint32_t slot_base;  // leaf slots are absolute positions in the shared order array
   std::vector<uint32_t> idx[3];
   std::vector<uint8_t> on_left;  // by item id, scratch of one split
@@ -135,22 +137,21 @@ struct Builder {
   // parent split on (-1 at the root: list order).
   uint32_t build(uint32_t begin, uint32_t end, uint32_t depth, int pa) {
     const uint32_t n = end - begin;
-    if (n <= leaf_max) {
-      if (pa < 0) {  // a root leaf keeps list order (ids are list-ordered)
-        for (uint32_t i = 0; i < n; ++i) slots[begin + i] = begin + i;
-      } else {
-        for (uint32_t i = 0; i < n; ++i) slots[begin + i] = idx[pa][begin + i];
-      }
-      return bvh_leaf_ref(slot_base + begin, n);
-    }
+    if (n <= leaf_max) return leaf(begin, n, pa);
     Box3 cbox;
-    (void)bounds(idx[0].data() + begin, n, &cbox);
+    const Box3 box = bounds(idx[0].data() + begin, n, &cbox);
     // SAH while the subtree can still be finished below the cap by balanced splits
     // (a median split at depth d with d + levels(n) = kBvhStack leaves the deepest
     // internal node at kBvhStack - 1)
     int axis = -1;
     uint32_t mid = begin;
-    if (depth + balanced_levels(n, leaf_max) < kBvhStack) sah_split(begin, end, cbox, &axis, &mid);
+    double split = INFINITY;  // the chosen split's sum of (side area x count)
+    if (depth + balanced_levels(n, leaf_max) < kBvhStack) sah_split(begin, end, cbox, &axis, &mid, &split);
+    // SAH termination (sah_ct > 0): a leaf of up to leaf_cap items where testing them all
+    // costs no more than a node step (sah_ct leaf tests) plus the split's expected tests
+    if (sah_ct > 0.0 && n <= leaf_cap && split < INFINITY && box.area() > 0.0 &&
+        static_cast<double>(n) <= sah_ct + split / box.area())
+      return leaf(begin, n, pa);
     if (mid == begin || mid == end) median_split(begin, end, cbox, &axis, &mid);
     // ids of the left side first on every axis, each side in its axis order
     for (uint32_t i = begin; i < end; ++i) on_left[idx[axis][i]] = i < mid;
@@ -189,6 +190,16 @@ struct Builder {
     return at;
   }
 
+  // a leaf over range [begin, begin + n): its slots in the parent's split-axis order
+  uint32_t leaf(uint32_t begin, uint32_t n, int pa) {
+    if (pa < 0) {  // a root leaf keeps list order (ids are list-ordered)
+      for (uint32_t i = 0; i < n; ++i) slots[begin + i] = begin + i;
+    } else {
+      for (uint32_t i = 0; i < n; ++i) slots[begin + i] = idx[pa][begin + i];
+    }
+    return bvh_leaf_ref(slot_base + begin, n);
+  }
+
   static int longest(const Box3& cbox, float* ext_out) {
     int axis = 0;
     float ext = -1.0f;
@@ -215,7 +226,7 @@ struct Builder {
   // cheapest position. C5 trace 45.6 ms, against 46.5 for the sweep on the longest axis only
   // and 51.3 for 12 bins on the longest axis (8 bins 48.5, 16 bins 52.3: binned trees walked
   // at very different speeds; profiles/AB_LOG.md).
-  void sah_split(uint32_t begin, uint32_t end, const Box3& cbox, int* axis, uint32_t* mid) {
+  void sah_split(uint32_t begin, uint32_t end, const Box3& cbox, int* axis, uint32_t* mid, double* cost_out) {
     float ext;
     (void)longest(cbox, &ext);
     if (!(ext > 0.0f)) return;
@@ -230,6 +241,7 @@ struct Builder {
         *mid = begin + i;
       }
     }
+    *cost_out = best;
   }
 
   // the least-cost partition position of the range in axis k's order (0 if none)
@@ -298,6 +310,9 @@ bool build_range(const std::vector<fr_prim>& prims, uint32_t begin, uint32_t end
   if (nodes.size() + n >= kBvhLeaf) return false;
   std::vector<uint32_t> slots;
   Builder b(items, nodes, slots, pad, leaf_max, static_cast<uint32_t>(order.size()));
+  if (const char* e = getenv("FR_BVH_SAH_CT")) b.sah_ct = atof(e);  // A/B
+  if (const char* e = getenv("FR_BVH_LEAF_CAP"))
+    if (atoi(e) >= 1 && atoi(e) <= static_cast<int>(kBvhLeafCountMax)) b.leaf_cap = static_cast<uint32_t>(atoi(e));
   root = b.build(0, n, 0, -1);
   for (uint32_t id : slots) order.push_back(items[id].index);
   return true;
