@@ -610,7 +610,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   __syncthreads();
 
 
-  enum : uint32_t { NEED_NONE = 0, NEED_LENS = 1, NEED_SPHERE = 2 };
+  // NEED_JIT: a sample starts (its jitter, then its first lens try); NEED_LENS: a camera
+  // lane's lens try after a rejected one
+  enum : uint32_t { NEED_NONE = 0, NEED_LENS = 1, NEED_SPHERE = 2, NEED_JIT = 3 };
   uint32_t depth = 0;  // scatters of the path (not NIB: wnib holds them)
   // NIB: the winners as 4-bit entries, the last one pushed in bits 28..31 and the first in
   // bits 32 - 4 depth .. 35 - 4 depth, 15 on the levels below (empty). sum_kernel multiplies
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // (a lane needs a work item when its block's samples are done: s == s_end, both 0 at the
   // start, and a claim that finds no pixel leaves them equal; a compare the loop's ballot
   // takes directly, where a carried bool cost a select and a compare per iteration)
-  bool active = true, need_jit = false, have_ray = false;
+  bool active = true, have_ray = false;
   uint32_t need = NEED_NONE;
 
 #ifdef FR_PROF
@@ -808,24 +810,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           s_end = min(s + (fine ? kFineSamples : kBlockSamples), kp.spp);
           fx = static_cast<float>(x) * 16777216.0f;  // 2^24 x, exact (x, yrow < 2^24)
           fy = static_cast<float>(yrow) * 16777216.0f;
-          need_jit = true;
+          need = NEED_JIT;  // a sample starts: its jitter and lens sample in step 1
         }
       }
-    }
-    if (need_jit) {
-      SEC(SC_JIT);
-      // a sample starts: jitter (tracer.rs:171-172), then its lens sample in step 1. One
-      // place for the first sample of a block and the next sample of the same block, so
-      // the wave runs it once per iteration
-      // 2^24 (x + r) = RN(2^24 x + 2^24 r) (rounding commutes with the exact scaling), so
-      // the quotients are (x + r) / W's bits: numerator +0 or in [1, 2^56], divisor 2^24 W
-      const float r0 = rng_f32_scaled(rng);
-      const float r1 = rng_f32_scaled(rng);
-      d.x = div_rn(fx + r0, kp.sW, kp.rW);
-      d.y = div_rn(fy + r1, kp.sH, kp.rH);
-      if (MT) d.y = d.y + vofs;  // render_mt's band offset (tracer.rs:103)
-      need = NEED_LENS;
-      need_jit = false;
     }
     PROF_MARK(PF_CLAIM);
     bool ended = false;
@@ -850,7 +837,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       // the test in the 2^23-scaled domain (rng_signed_unit_scaled): same decisions
       float px = rng_signed_unit_scaled(rng);
       float py = rng_signed_unit_scaled(rng);
-      if (lane_in(msph)) pz = rng_signed_unit_scaled(rng);
+      // A sample's first draws are its jitter (tracer.rs:171-172), then its lens try: a
+      // starting lane's first try takes four draws where a scatter lane's takes three (and a
+      // camera lane's retry two). The third draw is made by both kinds in one instruction
+      // sequence; a starting lane's first two are its jitter and it draws its try's fourth
+      // in the branch below (the jitter's own two draws in their own branch, in the quarter
+      // of lanes that start a sample, cost a branch of 31 VALU)
+      const unsigned long long mjit = __builtin_amdgcn_ballot_w64(need == NEED_JIT);
+      float pw = 0.0f;
+      if (lane_in(msph | mjit)) pw = rng_signed_unit_scaled(rng);
+      if (lane_in(msph)) pz = pw;
+      if (lane_in(mjit)) {
+        SEC(SC_JIT);
+        // 2^24 r = (int32)u >> 8 + 2^23 (rng_f32_scaled; exact). 2^24 (x + r) = RN(2^24 x +
+        // 2^24 r) (rounding commutes with the exact scaling), so the quotients are
+        // (x + r) / W's bits: numerator +0 or in [1, 2^56], divisor 2^24 W
+        d.x = div_rn(fx + (px + 8388608.0f), kp.sW, kp.rW);
+        d.y = div_rn(fy + (py + 8388608.0f), kp.sH, kp.rH);
+        if (MT) d.y = d.y + vofs;  // render_mt's band offset (tracer.rs:103)
+        px = pw;
+        py = rng_signed_unit_scaled(rng);
+        need = NEED_LENS;
+      }
       float dd = px * px + py * py + pz * pz;
       unsigned long long mrej = __builtin_amdgcn_ballot_w64(dd >= kUnitBallScaled);
       while (lanes_in(mrej) > static_cast<uint32_t>(KREJ)) {
@@ -1520,7 +1528,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #ifdef FR_DIAG
       if (s + 1u == s_end && diag_tb < (1u << 20)) atomicAdd(&g_fr_tb_cost[diag_tb], nseg - diag_seg0);
 #endif
-      if (++s != s_end) need_jit = true;  // next sample of the block, same stream (else: a new item)
+      if (++s != s_end) need = NEED_JIT;  // next sample of the block, same stream (else: a new item)
     }
     PROF_MARK(PF_END);
     SEC(SC_LATCH);
