@@ -922,6 +922,8 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   kc.ux = cam->u[0], kc.uy = cam->u[1], kc.uz = cam->u[2];
   kc.bx = cam->v[0], kc.by = cam->v[1], kc.bz = cam->v[2];
   kc.lens = cam->lens_radius;
+  kc.lens_s = ldexpf(kc.lens, -23);
+  kc.lens_pre = std::isfinite(kc.lens) && ldexpf(kc.lens_s, 23) == kc.lens ? 1u : 0u;
   KParams kp;
   kp.W = p->width;
   kp.H = p->height;

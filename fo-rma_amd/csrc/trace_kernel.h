@@ -211,8 +211,10 @@ struct KWork {
 // horizontal, vertical, u, v (named b* here), lens_radius
 struct KCam {
   float px, py, pz, lx, ly, lz, hx, hy, hz, vx, vy, vz, ux, uy, uz, bx, by, bz, lens;
+  float lens_s;       // lens 2^-23
+  uint32_t lens_pre;  // lens_s is exact (no underflow): the lens sample uses it
 };
-static_assert(sizeof(KCam) == 19 * 4, "KCam is 19 floats");
+static_assert(sizeof(KCam) == 21 * 4, "KCam is 21 words");
 
 struct KArgs {
   KScene sc;
@@ -875,9 +877,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       }
       SEC(SC_ACC);
       if (!lane_in(mrej)) {
-        px *= kSignedUnitScale;  // the accepted point, 2r - 1 per coordinate (exact)
-        py *= kSignedUnitScale;
-        pz *= kSignedUnitScale;
+        // the accepted point is k 2^-23 per coordinate (2r - 1, exact), k = (px, py, pz):
+        // the scale is folded into the operation that uses it (below)
         if (!lane_in(msph)) {
           SEC(SC_CAM);
           // Camera::get_ray (camera.rs:62-72)
@@ -894,7 +895,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #endif
           const V3 cpos{cm.px, cm.py, cm.pz}, cllc{cm.lx, cm.ly, cm.lz}, chor{cm.hx, cm.hy, cm.hz};
           const V3 cver{cm.vx, cm.vy, cm.vz}, cu{cm.ux, cm.uy, cm.uz}, cv{cm.bx, cm.by, cm.bz};
-          const V3 rd = scl(cm.lens, V3{px, py, 0.0f});
+          // lens * (k 2^-23) = (lens 2^-23) * k when lens 2^-23 is exact (KCam::lens_pre):
+          // the same product, one rounding
+          const V3 rd = cm.lens_pre ? V3{cm.lens_s * px, cm.lens_s * py, 0.0f}
+                                    : scl(cm.lens, V3{px * kSignedUnitScale, py * kSignedUnitScale, 0.0f});
           const V3 off = add(scl(rd.x, cu), scl(rd.y, cv));
           const float u = d.x, v = d.y;
           o = add(cpos, off);
@@ -903,14 +907,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           have_ray = true;
         } else {
           SEC(SC_SCAT);
-          const V3 r{px, py, pz};
           bool ok = true;
           V3 dir;
           if (!DIFFUSE && smetal) {
+            const V3 r{px * kSignedUnitScale, py * kSignedUnitScale, pz * kSignedUnitScale};
             dir = add(d, scl(sfuzz, r));  // reflected + fuzz * rus
             ok = dot(dir, sn) > 0.0f;     // sphere.rs:104 / plane.rs:121
           } else {
-            dir = sub(add(d, r), o);  // ((p + n) + rus) - p
+            // ((p + n) + rus) - p; p + n + k 2^-23 as one fma (the product is exact)
+            const V3 dr{__builtin_fmaf(px, kSignedUnitScale, d.x), __builtin_fmaf(py, kSignedUnitScale, d.y),
+                        __builtin_fmaf(pz, kSignedUnitScale, d.z)};
+            dir = sub(dr, o);
           }
           if (ok) {
             if (!(NIB && DIFFUSE)) push(sbest);  // (NIB && DIFFUSE kernels pushed at the shading step)
