@@ -810,8 +810,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
           diag_seg0 = nseg;
 #endif
           s_end = min(s + (fine ? kFineSamples : kBlockSamples), kp.spp);
-          fx = static_cast<float>(x) * 16777216.0f;  // 2^24 x, exact (x, yrow < 2^24)
-          fy = static_cast<float>(yrow) * 16777216.0f;
+          // 2^24 x + 2^23, exact (x, yrow < 2^23): the jitter's numerator base (step 1)
+          fx = static_cast<float>(x) * 16777216.0f + 8388608.0f;
+          fy = static_cast<float>(yrow) * 16777216.0f + 8388608.0f;
           need = NEED_JIT;  // a sample starts: its jitter and lens sample in step 1
         }
       }
@@ -851,11 +852,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
       if (lane_in(msph)) pz = pw;
       if (lane_in(mjit)) {
         SEC(SC_JIT);
-        // 2^24 r = (int32)u >> 8 + 2^23 (rng_f32_scaled; exact). 2^24 (x + r) = RN(2^24 x +
-        // 2^24 r) (rounding commutes with the exact scaling), so the quotients are
-        // (x + r) / W's bits: numerator +0 or in [1, 2^56], divisor 2^24 W
-        d.x = div_rn(fx + (px + 8388608.0f), kp.sW, kp.rW);
-        d.y = div_rn(fy + (py + 8388608.0f), kp.sH, kp.rH);
+        // 2^24 r = (int32)u >> 8 + 2^23 (rng_f32_scaled; exact), so 2^24 x + 2^24 r =
+        // (2^24 x + 2^23) + px, one rounding either way. 2^24 (x + r) = RN(2^24 x + 2^24 r)
+        // (rounding commutes with the exact scaling), so the quotients are (x + r) / W's
+        // bits: numerator +0 or in [1, 2^56], divisor 2^24 W
+        d.x = div_rn(fx + px, kp.sW, kp.rW);
+        d.y = div_rn(fy + py, kp.sH, kp.rH);
         if (MT) d.y = d.y + vofs;  // render_mt's band offset (tracer.rs:103)
         px = pw;
         py = rng_signed_unit_scaled(rng);
