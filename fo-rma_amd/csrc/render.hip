@@ -1077,7 +1077,8 @@ static int render_impl(fr_ctx* c, fr_scene* scene, const fr_camera* cam, const f
   const size_t stage_n = stage_samples(use_bvh, nibble);
   const size_t lds = (stage_n > 1 && (!use_bvh || nibble) ? kBlock * stage_n * wps * sizeof(float) : 0u) +
                      (n_att ? n_att + 1 : 0) * 16 +
-                     n_rec * 64 + stack_bytes + (use_bvh ? dc->bvh_levels * kBlock * sizeof(uint32_t) : 0u);
+                     n_rec * 64 + stack_bytes +
+                     (use_bvh ? (dc->bvh_levels + 1u) * kBlock * sizeof(uint32_t) : 0u);  // + the sentinel row
   // the scene-specialised kernel (jit.h): list-loop scenes of <= kJitMaxPrims primitives,
   // when the caller asks (FR_FLAG_SCENE_JIT; FR_SCENE_JIT=1 / 0 forces it on / off)
   JitReq jr;

@@ -396,6 +396,13 @@ __device__ __forceinline__ unsigned long long lanes_lt_u32(uint32_t v, uint32_t 
   return v < s;  // device only
 #endif
 }
+// LDS byte address of a pointer into __shared__ memory, and the u32 at such an address
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint32_t*)p));
+}
+__device__ __forceinline__ __attribute__((address_space(3))) uint32_t& lds_u32_at(uint32_t a) {
+  return *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(static_cast<uintptr_t>(a));
+}
 __device__ __forceinline__ uint32_t lane_sel(unsigned long long m, uint32_t if_set, uint32_t if_clear) {
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t r;
@@ -581,6 +588,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
   // BVH traversal stack, after the unwind stack: kBvhStack x kBlock u32 (level-major)
   // (8-B-record kernels keep their winners in a register: no unwind stack in front)
   uint32_t* tstack = stack + (NIB ? 0u : MAXD ? (MAXD * kBlock) / 2u : (kp.max_depth ? kp.max_depth : 1u) * kBlock);
+  // ... addressed by LDS byte address. Its first level is a sentinel row of kBvhEnd below
+  // level 0, so that the top of an empty stack reads kBvhEnd: a pop needs no empty test.
+  // tbase: level 0's first entry
+  constexpr uint32_t kLevelB = 4u * kBlock;
+  const uint32_t tbase = lds_addr(tstack) + kLevelB;
+  if (BVH) tstack[tid] = kBvhEnd;  // (each lane reads only its own column)
   // MAXD > 0 stack entries: with the attenuations in LDS, the entry's byte offset in
   // att_lds (n_att <= kAttLds, so < 2^16), read by the unwind without index arithmetic;
   // otherwise the primitive index
@@ -994,9 +1007,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
             continue;
           }
           uint32_t ref = sp[1];
-          // this lane's next free traversal-stack entry, an index into tstack (level-major:
-          // one level is kBlock entries); the stack is empty while it is in level 0
-          uint32_t tso = tid;
+          // this lane's next free traversal-stack entry as its LDS byte address (level-major:
+          // one level is kBlock entries, kLevelB bytes); the stack is empty while it is in
+          // level 0, and the entry below it is the sentinel row. (As an index, every read and
+          // write cost an address add.)
+          uint32_t tso = tbase + 4u * tid;
           // node slabs as fma(lo, inv, -o inv): a cull only, covered by the padding for
           // origins within kBvhOriginReach scene extents (bvh.h; the host checks the camera).
           // The cull's reciprocal is clamped to +-2^100 (bvh.h kBvhInvClamp): an exact-zero
@@ -1030,17 +1045,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                 if (depth == 0) DIAG_LANE(DG_NPRIM_L);
               }
 #endif
-              // the stack's top, read before the node arrives (level 0's own entry, unused,
-              // when the stack is empty)
+              // the stack's top, read before the node arrives (the sentinel kBvhEnd when the
+              // stack is empty)
               typedef unsigned long long Mask;  // lane masks (ballots of single compares)
-              // (the compare in asm: the compiler fused it with tso - kBlock into a borrow,
-              // materialised as 0/1 and compared again for the ballot)
-              const uint32_t tdown = tso - kBlock;
-              const Mask mempty = lanes_lt_u32(tso, kBlock);
-              const uint32_t top = tstack[lane_sel(mempty, tso, tdown)];
+              const uint32_t tdown = tso - kLevelB;
+              const uint32_t top = lds_u32_at(tdown);
               // internal node: both children's boxes; the nearer entered child next (the
               // left one on a tie) and the other stacked when both are entered; neither: the
-              // stack's top. Branch-free: the far child is written to the free entry either
+              // stack's top (which ends the walk at the sentinel). Branch-free: the far child is written to the free entry either
               // way (a node at depth d has at most d entries below it, d < kBvhStack) and the
               // index moves only on a push or pop. (A ballot of an & of compares went through
               // a 0/1 VGPR and a compare: the compares' own masks are combined with SALU ops.)
@@ -1056,10 +1068,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                 // copied to a VGPR first (one scalar operand per VALU instruction)
                 const uint32_t cx = cl ^ cr;
                 const uint32_t near = cl ^ lane_sel(mgol, 0u, cx);
-                tstack[tso] = near ^ cx;  // the far child
-                const uint32_t tpop = lane_sel(many | mempty, tso, tdown);
-                ref = lane_sel(many, near, lane_sel(mempty, kBvhEnd, top));
-                tso = lane_sel(ml & mr, tso + kBlock, tpop);
+                lds_u32_at(tso) = near ^ cx;  // the far child
+                const uint32_t tpop = lane_sel(many, tso, tdown);
+                ref = lane_sel(many, near, top);
+                tso = lane_sel(ml & mr, tso + kLevelB, tpop);
               };
               auto node_step = [&](const float4 na, const float4 nb, const float4 nc, const uint32_t cl,
                                    const uint32_t cr) {
@@ -1157,11 +1169,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               }
               asm volatile("; bvh leaf: vector");
             }
-            {
-              const bool empty = tso < kBlock;
-              if (!empty) tso -= kBlock;
-              ref = empty ? kBvhEnd : tstack[tso];
-            }
+            tso -= kLevelB;  // pop (the sentinel kBvhEnd when the stack was empty)
+            ref = lds_u32_at(tso);
           }
         }
       }
