@@ -407,10 +407,20 @@ FR_HD Slab slab3(V3 lo, V3 hi, V3 o, V3 inv) {
 
 // The same slab distances as fma(lo, inv, -o inv) with oinv = o inv precomputed: not
 // the box primitive's exact arithmetic, only for the BVH's padded cull boxes (bvh.h).
+// One slab distance fma(c, inv, -oinv). A plane at a compile-time 0 (the scene kernel's
+// constants) is -oinv: 0 * inv is a zero for the finite (clamped) inv of the box test and the
+// cull, so the two differ at most in the sign of a zero distance, which neither root
+// selection (t > t_min) nor the face test (t equal to a distance) can see.
+FR_HD float slab_d(float c, float inv, float oinv) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (__builtin_constant_p(c) && c == 0.0f) return -oinv;
+#endif
+  return fmaf(c, inv, -oinv);
+}
 FR_HD Slab slab3_fused(V3 lo, V3 hi, V3 oinv, V3 inv) {
   Slab s;
-  s.t0 = V3{fmaf(lo.x, inv.x, -oinv.x), fmaf(lo.y, inv.y, -oinv.y), fmaf(lo.z, inv.z, -oinv.z)};
-  s.t1 = V3{fmaf(hi.x, inv.x, -oinv.x), fmaf(hi.y, inv.y, -oinv.y), fmaf(hi.z, inv.z, -oinv.z)};
+  s.t0 = V3{slab_d(lo.x, inv.x, oinv.x), slab_d(lo.y, inv.y, oinv.y), slab_d(lo.z, inv.z, oinv.z)};
+  s.t1 = V3{slab_d(hi.x, inv.x, oinv.x), slab_d(hi.y, inv.y, oinv.y), slab_d(hi.z, inv.z, oinv.z)};
   s.tn = fmax3_num(fmin_num(s.t0.x, s.t1.x), fmin_num(s.t0.y, s.t1.y), fmin_num(s.t0.z, s.t1.z));
   s.tf = fmin3_num(fmax_num(s.t0.x, s.t1.x), fmax_num(s.t0.y, s.t1.y), fmax_num(s.t0.z, s.t1.z));
   return s;

@@ -350,7 +350,7 @@ enum { PF_CLAIM, PF_REJ, PF_HIT, PF_SHADE, PF_END, PF_N };
 // (counters[32 + k]).
 enum { SC_ITER, SC_CLAIM, SC_JIT, SC_NEED, SC_REJ, SC_CAM, SC_SCAT, SC_HIT, SC_SKY, SC_SHADE, SC_END, SC_NODE,
        SC_LEAF, SC_NODES, SC_NODEV, SC_LTESTS, SC_LTESTV, SC_LIST, SC_LROOT, SC_N, SC_GRAB = SC_N, SC_SETUP, SC_ACC, SC_POSTHIT,
-       SC_POSTSHADE, SC_LATCH };
+       SC_POSTSHADE, SC_LATCH, SC_NODET };
 #if defined(FR_SEC_MARKS) && defined(__HIP_DEVICE_COMPILE__)
 #define SEC(k) asm volatile(";FRSEC " #k)
 #elif defined(FR_SECCNT)
@@ -1050,11 +1050,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               typedef unsigned long long Mask;  // lane masks (ballots of single compares)
               const uint32_t tdown = tso - kLevelB;
               const uint32_t top = lds_u32_at(tdown);
+              // the step's outcome, applied after the scalar or vector path (each path doing it
+              // itself left a register copy of the stack position at the loop's latch)
+              uint32_t t_near, t_far;
+              Mask t_many, t_both;
               // internal node: both children's boxes; the nearer entered child next (the
               // left one on a tie) and the other stacked when both are entered; neither: the
-              // stack's top (which ends the walk at the sentinel). Branch-free: the far child is written to the free entry either
-              // way (a node at depth d has at most d entries below it, d < kBvhStack) and the
-              // index moves only on a push or pop. (A ballot of an & of compares went through
+              // stack's top (the sentinel ends the walk). Branch-free: the far child is written
+              // to the free entry either way (a node at depth d has at most d entries below it,
+              // d < kBvhStack) and the index moves only on a push or pop. (A ballot of an & of compares went through
               // a 0/1 VGPR and a compare: the compares' own masks are combined with SALU ops.)
               auto node_pick = [&](const Slab& sl, const Slab& sr, const uint32_t cl, const uint32_t cr) {
                 const Mask ml = __builtin_amdgcn_ballot_w64(sl.tn <= sl.tf) &
@@ -1068,10 +1072,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                 // copied to a VGPR first (one scalar operand per VALU instruction)
                 const uint32_t cx = cl ^ cr;
                 const uint32_t near = cl ^ lane_sel(mgol, 0u, cx);
-                lds_u32_at(tso) = near ^ cx;  // the far child
-                const uint32_t tpop = lane_sel(many, tso, tdown);
-                ref = lane_sel(many, near, top);
-                tso = lane_sel(ml & mr, tso + kLevelB, tpop);
+                t_near = near;
+                t_far = near ^ cx;
+                t_many = many;
+                t_both = ml & mr;
               };
               auto node_step = [&](const float4 na, const float4 nb, const float4 nc, const uint32_t cl,
                                    const uint32_t cr) {
@@ -1081,8 +1085,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #if FR_BVH_SCALAR_NODES
               const uint32_t ref0 = __builtin_amdgcn_readfirstlane(ref);
               if (__ballot(ref != ref0) == 0) {
-                // every walking lane is at the same node (a quarter of C5's node steps, primary
-                // rays of one tile): scalar loads, the slab arithmetic on SGPR operands (the
+                // every walking lane is at the same node (90 % of C5's node steps): scalar loads, the slab arithmetic on SGPR operands (the
                 // distinct asm ends keep the two paths from being merged over copies of the
                 // node into VGPRs)
                 const RecRef nd = rec_at(sc.bvh, ref0);
@@ -1099,6 +1102,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
                 node_step(buf_load4(sc.bvh, nb0), buf_load4(sc.bvh, nb0 + 16u), buf_load4(sc.bvh, nb0 + 32u), nr.x, nr.y);
                 asm volatile("; bvh node step: vector");
               }
+              SEC(SC_NODET);
+              lds_u32_at(tso) = t_far;  // the far child
+              const uint32_t tpop = lane_sel(t_many, tso, tdown);
+              ref = lane_sel(t_many, t_near, top);
+              tso = lane_sel(t_both, tso + kLevelB, tpop);
             }
             if (ref == kBvhEnd) break;
             SEC(SC_LEAF);

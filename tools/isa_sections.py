@@ -32,7 +32,7 @@ REGIONS = ["SC_ITER", "SC_CLAIM", "SC_JIT", "SC_NEED", "SC_REJ", "SC_CAM", "SC_S
            "SC_END", "SC_NODE", "SC_LEAF", "SC_NODES", "SC_NODEV", "SC_LTESTS", "SC_LTESTV", "SC_LIST", "SC_LROOT"]
 # marker-only regions: the counted region whose entries they share
 DERIVED = {"SC_SETUP": "SC_CLAIM", "SC_ACC": "SC_NEED", "SC_POSTHIT": "SC_HIT", "SC_POSTSHADE": "SC_ITER",
-           "SC_LATCH": "SC_ITER"}
+           "SC_LATCH": "SC_ITER", "SC_NODET": "SC_NODE"}
 # render.hip jit_defines() for the default build
 DEFINES = dict(FR_KREJ=4, FR_KREJ_NIB=9, FR_CLAIM_MIN=1, FR_CLAIM_MIN_NIB=3, FR_NUM_SGPR=96, FR_BLOCK_SAMPLES=16,
                FR_FINE_SAMPLES=4, FR_STAGE=4, FR_BVH_STAGE=2, FR_NIB_WAVES=8, FR_DIFF12_WAVES=7)
