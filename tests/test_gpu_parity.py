@@ -1078,6 +1078,24 @@ def test_bvh_far_scene_axis_parallel_bounces(gpu, monkeypatch):
     assert np.array_equal(mean0.view(np.uint32), mean.view(np.uint32)) and st0["hits"] == st["hits"]
 
 
+@pytest.mark.parametrize("aperture", [0.0, 0.1, 2e-30, 1e-33, 3.0])
+def test_lens_radius_prescale_and_its_fallback(gpu, aperture):
+    """camera.rs:62-66's lens offset: the trace kernel multiplies the accepted disk point's
+    integers k by lens * 2^-23 when that product is exact (render.hip, KCam::lens_pre) and
+    scales k by 2^-23 first otherwise (aperture 1e-33: lens * 2^-23 underflows); a zero, a
+    tiny, the scenes' and a large aperture, both trace kernels, against the oracle bit for bit."""
+    name, w, h, spp, depth = "scene_08", 48, 27, 4, 8
+    sc = gpu.Scene.from_file(gpu.scene_path(name), w, h)
+    prims, (frm, at, vup, fov) = S.load_json(open(gpu.scene_path(name)).read())
+    cam = gpu.camera_look(frm, at, vup, fov, aperture, w, h)
+    omean, ou8, ocnt, _ = O.render(prims, O.camera_look(frm, at, vup, fov, aperture, w, h), w, h, spp, depth,
+                                   seed=7, threads=8)
+    for jit in (False, "wait"):
+        mean, u8, st = gpu.render(sc, cam, w, h, spp, depth, seed=7, scene_jit=jit)
+        assert_parity(mean, u8, st, omean, ou8, ocnt)
+        assert np.array_equal(mean.view(np.uint32), omean.view(np.uint32))
+
+
 # ---- save_image_mt (tracer.rs:83-158) ---------------------------------------------
 
 @pytest.mark.parametrize("which,w,h,sample", [(0, 32, 18, 3), (0, 40, 24, 1), (2, 36, 22, 20), (0, 16, 3, 2)])
