@@ -383,19 +383,6 @@ __device__ __forceinline__ uint32_t lanes_in(unsigned long long m) {
 }
 __device__ __forceinline__ uint32_t lanes_set(bool b) { return lanes_in(__builtin_amdgcn_ballot_w64(b)); }
 
-// Per-lane select on a lane mask (a ballot): one v_cndmask_b32. The compiler turned chains
-// of selects on compare results into branches with the conditions materialised as 0/1
-// values in VGPRs; masks combined with SALU ops and this select keep them in SGPRs.
-// Lanes whose v < s (unsigned), as a lane mask.
-__device__ __forceinline__ unsigned long long lanes_lt_u32(uint32_t v, uint32_t s) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  unsigned long long m;
-  asm("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(m) : "s"(s), "v"(v));
-  return m;
-#else
-  return v < s;  // device only
-#endif
-}
 // LDS byte address of a pointer into __shared__ memory, and the u32 at such an address
 __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
   return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint32_t*)p));
@@ -403,6 +390,9 @@ __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
 __device__ __forceinline__ __attribute__((address_space(3))) uint32_t& lds_u32_at(uint32_t a) {
   return *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(static_cast<uintptr_t>(a));
 }
+// Per-lane select on a lane mask (a ballot): one v_cndmask_b32. The compiler turned chains
+// of selects on compare results into branches with the conditions materialised as 0/1
+// values in VGPRs; masks combined with SALU ops and this select keep them in SGPRs.
 __device__ __forceinline__ uint32_t lane_sel(unsigned long long m, uint32_t if_set, uint32_t if_clear) {
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t r;
@@ -1058,8 +1048,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               // left one on a tie) and the other stacked when both are entered; neither: the
               // stack's top (the sentinel ends the walk). Branch-free: the far child is written
               // to the free entry either way (a node at depth d has at most d entries below it,
-              // d < kBvhStack) and the index moves only on a push or pop. (A ballot of an & of compares went through
-              // a 0/1 VGPR and a compare: the compares' own masks are combined with SALU ops.)
+              // d < kBvhStack) and the index moves only on a push or pop. (A ballot of an & of
+              // compares went through a 0/1 VGPR and a compare: the compares' own masks are
+              // combined with SALU ops.)
               auto node_pick = [&](const Slab& sl, const Slab& sr, const uint32_t cl, const uint32_t cr) {
                 const Mask ml = __builtin_amdgcn_ballot_w64(sl.tn <= sl.tf) &
                                 __builtin_amdgcn_ballot_w64(sl.tf >= 0.001f) & __builtin_amdgcn_ballot_w64(sl.tn <= closest);
@@ -1085,9 +1076,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
 #if FR_BVH_SCALAR_NODES
               const uint32_t ref0 = __builtin_amdgcn_readfirstlane(ref);
               if (__ballot(ref != ref0) == 0) {
-                // every walking lane is at the same node (90 % of C5's node steps): scalar loads, the slab arithmetic on SGPR operands (the
-                // distinct asm ends keep the two paths from being merged over copies of the
-                // node into VGPRs)
+                // every walking lane is at the same node (90 % of C5's node steps): scalar
+                // loads, the slab arithmetic on SGPR operands (the distinct asm ends keep the
+                // two paths from being merged over copies of the node into VGPRs)
                 const RecRef nd = rec_at(sc.bvh, ref0);
                 const float4 r = nd[3];
                 SEC(SC_NODES);
