@@ -399,9 +399,15 @@ static int upload_scene(fr_scene* s, int device, DeviceCopy** out) {
     const float4 a = k < aclass.size() ? aclass[k] : make_float4(1.0f, 1.0f, 1.0f, 0.0f);
     memcpy(&host[c->off_acls_att + 16 * k], &a, 16);
   }
-  // the BVH leaves' records, in leaf-slot order
-  for (size_t slot = 0; slot < bvh_order.size(); ++slot)
-    memcpy(&host[c->off_lrec + 64 * slot], &host[c->off_rec + 64 * static_cast<size_t>(bvh_order[slot])], 64);
+  // the BVH leaves' records, in leaf-slot order; a sphere's carries RN(radius^2) in place of
+  // its radius, the product its hit test forms (sphere.rs:34; one VALU per leaf test saved)
+  for (size_t slot = 0; slot < bvh_order.size(); ++slot) {
+    float* lr = reinterpret_cast<float*>(&host[c->off_lrec + 64 * slot]);
+    memcpy(lr, &host[c->off_rec + 64 * static_cast<size_t>(bvh_order[slot])], 64);
+    uint32_t kind;
+    memcpy(&kind, &lr[15], 4);
+    if (kind == FR_SPHERE) lr[3] = lr[3] * lr[3];
+  }
   {
     // entry n: the unit attenuation the depth-8 stack's empty levels point at
     const float4 one = make_float4(1.0f, 1.0f, 1.0f, 0.0f);

@@ -181,10 +181,12 @@ FR_HD V3 random_in_unit_sphere(Rng& r) {
 
 // shapes/sphere.rs:23-51 without the record writes; a = dot(d, d) (loop-invariant).
 // Both roots are formed unconditionally (no side effects) and the near one wins.
-FR_HD bool sphere_root(V3 c, float radius, V3 o, V3 d, float a, float t_min, float t_max, float& t) {
+// rr = RN(radius * radius), the product the test forms (the BVH's leaf records carry it in
+// place of the radius, render.hip)
+FR_HD bool sphere_root_rr(V3 c, float rr, V3 o, V3 d, float a, float t_min, float t_max, float& t) {
   const V3 oc = sub(o, c);
   const float b = dot(oc, d);
-  const float cc = dot(oc, oc) - radius * radius;
+  const float cc = dot(oc, oc) - rr;
   const float disc = b * b - a * cc;
   if (disc > 0.0f) {
     const float sq = sqrtf(disc);
@@ -196,6 +198,9 @@ FR_HD bool sphere_root(V3 c, float radius, V3 o, V3 d, float a, float t_min, flo
     return c1 || c2;
   }
   return false;
+}
+FR_HD bool sphere_root(V3 c, float radius, V3 o, V3 d, float a, float t_min, float t_max, float& t) {
+  return sphere_root_rr(c, radius * radius, o, d, a, t_min, t_max, t);
 }
 
 // shapes/plane.rs:24-44. denom is compared against the t-range; when it passes,
@@ -340,11 +345,14 @@ __device__ __forceinline__ SphereSeg sphere_seg(float a) {
 struct SphereDisc {
   float b, disc;
 };
-__device__ __forceinline__ SphereDisc sphere_disc(V3 c, float radius, V3 o, V3 d, float a) {
+__device__ __forceinline__ SphereDisc sphere_disc_rr(V3 c, float rr, V3 o, V3 d, float a) {
   const V3 oc = sub(o, c);
   const float b = dot(oc, d);
-  const float cc = dot(oc, oc) - radius * radius;
+  const float cc = dot(oc, oc) - rr;
   return SphereDisc{b, b * b - a * cc};
+}
+__device__ __forceinline__ SphereDisc sphere_disc(V3 c, float radius, V3 o, V3 d, float a) {
+  return sphere_disc_rr(c, radius * radius, o, d, a);
 }
 // the roots of a sphere test whose discriminant is > 0
 __device__ __forceinline__ bool sphere_roots_fast(SphereDisc q, float a, SphereSeg sg, float t_min, float t_max,

@@ -1112,15 +1112,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(FR_NUM_SGPR)
               float t = 0.0f;
               bool h = false;
               if (k == FR_SPHERE) {
-                const float4 g = r[0];
+                const float4 g = r[0];  // centre, RN(radius^2) (the leaf records' form)
 #ifndef FR_SPHERE_IEEE
-                const SphereDisc q = sphere_disc(xyz(g), g.w, o, d, a_dd);
+                const SphereDisc q = sphere_disc_rr(xyz(g), g.w, o, d, a_dd);
                 if (q.disc > 0.0f) {
                   SEC(SC_LROOT);
                   h = sphere_roots_fast(q, a_dd, ssg, 0.001f, tmax, t);
                 }
 #else
-                h = sphere_root(xyz(g), g.w, o, d, a_dd, 0.001f, tmax, t);
+                h = sphere_root_rr(xyz(g), g.w, o, d, a_dd, 0.001f, tmax, t);
 #endif
               } else if (k == FR_AABB) {
                 h = slab_root(slab3_box(xyz(r[0]), xyz(r[1]), o, inv, boinv), 0.001f, tmax, t);
