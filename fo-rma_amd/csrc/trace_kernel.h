@@ -74,9 +74,10 @@ constexpr uint32_t kMaxWgPerCu = 8;   // 2048 threads per CU / kBlock: the persi
 #ifndef FR_CLAIM_MIN_NIB
 #define FR_CLAIM_MIN_NIB 3
 #endif
-// ... for the BVH kernels with 8-B attenuation-class records (A/B knobs; C5)
+// ... for the BVH kernels with 8-B attenuation-class records: C5 trace 39.51 -> 39.17 ms at 2
+// (0: 39.87, 1: 39.27, 3: 39.31, 6: 40.14; profiles/r06af_ab_c5_krej.log, four runs)
 #ifndef FR_KREJ_BVH
-#define FR_KREJ_BVH FR_KREJ
+#define FR_KREJ_BVH 2
 #endif
 #ifndef FR_CLAIM_MIN_BVH
 #define FR_CLAIM_MIN_BVH FR_CLAIM_MIN
